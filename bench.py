@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): LZ4 compress GB/s + JPEG DCT Gpixel/s
+on 1..8 MI355X, with % of the HBM roofline and the CPU path timed beside it.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+One JSON line on rank 0.  Top level = LZ4 (BASELINE.json configs[1]: 1 GiB of
+random_extract-style text per GPU, weak scaling: every rank compresses its own
+1 GiB shard of a global corpus, block-aligned); "jpeg" = configs[2] (one
+3840x2160 random RGB image per GPU per step).  A step is one pass of the hot
+path over one rank's batch with inputs resident in HBM; for N>1 it includes
+the all_gather of segment lengths (every rank learns its offset in the global
+stream).  The gatherv of all segments to rank 0 over RCCL is timed separately
+("lz4_gather_ms") because it moves output, not compute.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(REPO, "lz4-jpeg_amd"), os.path.join(REPO, "tests")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TOPS = 39.3     # 78.6 TFLOPS fp64 vector spec counts FMA as 2
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--lz4-bytes-per-rank", type=int, default=1 << 30)
+    ap.add_argument("--jpeg-w", type=int, default=3840)
+    ap.add_argument("--jpeg-h", type=int, default=2160)
+    ap.add_argument("--jpeg-images-per-rank", type=int, default=1)
+    ap.add_argument("--jpeg-steps", type=int, default=0, help="default: max(50, 10*steps)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-jpeg", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target wall time of each CPU-baseline sample")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from lz4jpeg import dist as ldist
+    from lz4jpeg import jpeg, lz4, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ------------------------------------------------------------------ LZ4
+    n_total = args.lz4_bytes_per_rank * world
+    lo, hi = ldist.shard_bytes(n_total, world, rank)
+    log(f"rank {rank}: synthesising LZ4 shard [{lo}, {hi}) of {n_total} B")
+    host = synth.random_passages(hi - lo, length=30000, seed=1, first=lo)
+    d_in = torch.from_numpy(host).to(dev)
+    n = hi - lo
+    comp = lz4.Compressor()
+    cap = lz4.compress_bound(n)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    d_len = torch.zeros(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def lz4_step():
+        if world == 1:
+            _, got = comp.compress_device(d_in, n, d_out)
+            return got
+        comp.compress_async(d_in, n, d_out, d_len, segment=True)
+        seg = int(d_len.item())
+        ldist.exchange_lengths(seg, dev)
+        return seg
+
+    for _ in range(args.warmup):
+        out_len = lz4_step()
+    torch.cuda.synchronize()
+    barrier()
+    comp.set_timing(True)
+    match_ms, call_ms = [], []
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out_len = lz4_step()
+        c_ms, m_ms = comp.last_timing()
+        call_ms.append(c_ms)
+        match_ms.append(m_ms)
+    torch.cuda.synchronize()
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    comp.set_timing(False)
+    lz4_ms = dt / args.steps * 1e3
+    lz4_gbs = n_total / (dt / args.steps) / 1e9
+    avg_match_ms = sum(match_ms) / len(match_ms)
+    avg_call_ms = sum(call_ms) / len(call_ms)
+    log(f"lz4: {lz4_ms:.3f} ms/step, {lz4_gbs:.1f} GB/s aggregate, analyze kernel "
+        f"{avg_match_ms:.3f} ms, call {avg_call_ms:.3f} ms, out {out_len} B")
+
+    gather_ms = None
+    if world > 1:
+        seg = lz4_step()
+        lens, offs = ldist.exchange_lengths(seg, dev)
+        torch.cuda.synchronize()
+        barrier()
+        g0 = time.perf_counter()
+        ldist.gather_stream(d_out, seg, ldist.nblocks(n_total), lens, offs, dst=0)
+        torch.cuda.synchronize()
+        barrier()
+        gather_ms = max_over_ranks(time.perf_counter() - g0) * 1e3
+
+    roof_lz4 = {
+        "bound": "hbm", "kernel": "lz4_analyze",
+        "achieved": round(n / (avg_match_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+        "unit": "GB/s", "frac": round(n / (avg_match_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "algorithmic_bytes_per_launch": n,
+        "avg_launch_ms": round(avg_match_ms, 4),
+        "whole_call_ms": round(avg_call_ms, 4),
+        "note": "algorithmic bytes = 1 B read per input byte (SURVEY §8d); HIP events on the "
+                "launch stream around lz4_analyze inside each timed step",
+    }
+
+    # ----------------------------------------------------------------- JPEG
+    jres = None
+    if not args.no_jpeg:
+        W, H, B = args.jpeg_w, args.jpeg_h, args.jpeg_images_per_rank
+        img = synth.rand_rgba(W, H, seed=1 + rank)
+        d_img = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(img, (B,) + img.shape))).to(dev)
+        d_coef = torch.empty(B * jpeg.coef_count(W, H), dtype=torch.int16, device=dev)
+        jsteps = args.jpeg_steps or max(50, 10 * args.steps)
+        for _ in range(max(args.warmup, 3)):
+            jpeg.encode_device(d_img, W, H, B, d_coef)
+        torch.cuda.synchronize()
+        barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(jsteps):
+            jpeg.encode_device(d_img, W, H, B, d_coef)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        barrier()
+        jdt = max_over_ranks(time.perf_counter() - t0)
+        kern_ms = ev0.elapsed_time(ev1) / jsteps
+        px_total = W * H * B * world
+        gpix = px_total / (jdt / jsteps) / 1e9
+        px_rank = W * H * B
+        tiles = ((W + 7) // 8) * ((H + 7) // 8) * B
+        jres = {
+            "metric": "JPEG DCT+quant+zigzag Gpixel/s (bit-exact int16 coefficients)",
+            "value": round(gpix, 3), "unit": "Gpixel/s", "n_gpus": world, "steps": jsteps,
+            "ms_per_step": round(jdt / jsteps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "dtype": "f64",
+            "data": "synthetic: glibc rand() RGBA noise (random_image.c), seed 1+rank",
+            "config": {"workload": "jpeg_encode_3840x2160_rgb", "w": W, "h": H,
+                       "images_per_rank": B, "parallelism": f"images{world}"},
+            "roofline": {
+                "bound": "hbm", "kernel": "jpeg_strip_kernel",
+                "achieved": round(8 * px_rank / (kern_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(8 * px_rank / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic": None, "algorithmic_bytes_per_launch": 8 * px_rank,
+                "avg_launch_ms": round(kern_ms, 4),
+                "binding_roof": {
+                    "bound": "valu_fp64", "unit": "Tops/s",
+                    "achieved": round(tiles * 13312 / (kern_ms / 1e3) / 1e12, 2),
+                    "peak": FP64_VALU_PEAK_TOPS,
+                    "frac": round(tiles * 13312 / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
+                    "note": "13312 non-fused fp64 mul/add per tile in reference order "
+                            "(8704 luma + 2x2304 chroma); peak = 78.6 TF fp64 vector spec / 2",
+                },
+                "note": "8 B/pixel algorithmic (4 B RGBA read + 4 B int16 written)",
+            },
+        }
+        log(f"jpeg: {jres['ms_per_step']} ms/step, {gpix:.2f} Gpix/s aggregate, kernel {kern_ms:.4f} ms")
+
+    # --------------------------------------------------------- CPU baselines
+    cpu_lz4 = cpu_jpeg = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_lz4, cpu_jpeg = cpu_baselines(host, args, None if args.no_jpeg else img)
+
+    if rank == 0:
+        line = {
+            "metric": "LZ4 compress GB/s + JPEG DCT Mpixel/s at 1/2/4/8 MI355X; % HBM roofline",
+            "value": round(lz4_gbs, 3), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(lz4_ms, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: random_extract-style 30000-B passages of Metamorphosis.txt, "
+                    "newlines->spaces, glibc rand seed 1; each rank synthesises its shard",
+            "config": {"workload": "lz4_compress_1GiB_text_per_gpu", "bytes_per_rank": n,
+                       "bytes_total": n_total, "block": 300, "parallelism": f"shard{world}",
+                       "compressed_bytes_rank0": out_len},
+            "roofline": roof_lz4,
+            "cpu_baseline": cpu_lz4,
+            "lz4_gather_ms": None if gather_ms is None else round(gather_ms, 3),
+            "jpeg": jres,
+        }
+        if jres is not None:
+            jres["cpu_baseline"] = cpu_jpeg
+        print(json.dumps(line), flush=True)
+    comp.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baselines(text, args, img):
+    """Reference-path CPU throughput on this host's cores (rank 0, N=1 only),
+    on bounded samples of the same workloads."""
+    import numpy as np
+    import oracle_api
+    threads = max(1, min(16, os.cpu_count() or 1))
+    o = oracle_api.load()
+    # LZ4: oracle port (the reference LZ4.c cannot be built: Windows <direct.h>)
+    calib = 2 << 20
+    scratch = np.empty((calib // 300 + 1) * o.L.lz4o_block_bound(), np.uint8)
+    t = time.perf_counter()
+    o.L.lz4o_encode_parallel(text.ctypes.data, calib, threads, scratch.ctypes.data)
+    rate = calib / max(time.perf_counter() - t, 1e-6)
+    sample = int(min(text.size, max(calib, rate * args.cpu_seconds)))
+    sample -= sample % 300
+    scratch = np.empty((sample // 300 + 1) * o.L.lz4o_block_bound(), np.uint8)
+    t = time.perf_counter()
+    o.L.lz4o_encode_parallel(text.ctypes.data, sample, threads, scratch.ctypes.data)
+    dt = time.perf_counter() - t
+    cpu_lz4 = {"value": round(sample / dt / 1e9, 5), "unit": "GB/s", "cores": threads,
+               "kind": "port", "sample": f"first {sample} B of the rank-0 1 GiB corpus, "
+               f"{threads} pthreads over contiguous 300-B block ranges, {dt:.2f} s"}
+    log(f"cpu lz4: {cpu_lz4}")
+    cpu_jpeg = None
+    if img is not None:
+        h, w = img.shape[:2]
+        ref = oracle_api.ref_jpeg()
+        band = 8 * ((h // 8 + threads - 1) // threads)
+        bands = [(y, min(h, y + band)) for y in range(0, h, band)]
+        out = np.empty(((w + 7) // 8) * ((h + 7) // 8) * 128, np.int16)
+
+        def run_band(y0, y1):
+            sub = np.ascontiguousarray(img[y0:y1])
+            o_sub = np.empty(((w + 7) // 8) * ((y1 - y0 + 7) // 8) * 128, np.int16)
+            if ref is not None:
+                ref.ref_jpeg_encode_image(sub.ctypes.data, w, y1 - y0, o_sub.ctypes.data)
+            else:
+                o.L.jo_encode_image(sub.ctypes.data, w, y1 - y0, o_sub.ctypes.data)
+            out[(y0 // 8) * ((w + 7) // 8) * 128:][:o_sub.size] = o_sub
+
+        t = time.perf_counter()
+        ths = [threading.Thread(target=run_band, args=b) for b in bands]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t
+        cpu_jpeg = {"value": round(w * h / dt / 1e9, 6), "unit": "Gpixel/s", "cores": len(bands),
+                    "kind": "reference" if ref is not None else "port",
+                    "sample": f"one {w}x{h} image in {len(bands)} tile-row bands on "
+                              f"{len(bands)} threads, {dt:.2f} s"
+                              + (" (reference JPEG.c built from its sources, oracle/_ref)"
+                                 if ref is not None else " (oracle port)")}
+        log(f"cpu jpeg: {cpu_jpeg}")
+    return cpu_lz4, cpu_jpeg
+
+
+if __name__ == "__main__":
+    main()

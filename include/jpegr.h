@@ -1,0 +1,74 @@
+/*
+ * jpegr.h -- C ABI of the MI355X JPEG hot path (colour conversion, 4:2:2
+ * odd-column subsampling, 8x8/8x4 tiling, fp64 DCT-II, truncating
+ * quantisation, zigzag), bit-exact to the reference's sequential C.
+ *
+ * Replaces, for a whole image (or a batch of images) at once, the reference's
+ * per-tile host loop in Algorithms/sequential/JPEG/JPEG.c:
+ *   build_luminance_matrix / build_rChrominance_matrix /
+ *   build_bChrominance_matrix   JPEG.c:114-185
+ *   chroma_subsample            JPEG.c:302-375
+ *   divide_image                JPEG.c:496-550
+ *   discrete_cosine_transform   JPEG.c:451-494
+ *   Quantize                    JPEG.c:621-629
+ *   zigzag_pattern              JPEG.c:693-728
+ *   (driven by main, JPEG.c:1110-1178)
+ *
+ * Input: RGBA8 pixels, row-major, 4 bytes/pixel (the reference's Pixel,
+ * JPEG.c:29-32; alpha ignored).  Output: per 8x8 tile, 128 int16
+ * little-endian = [Y 64 zigzag][Cr 32 zigzag][Cb 32 zigzag]; tiles in raster
+ * order (this layout is defined by this library: the reference keeps the
+ * quantised coefficients as doubles in memory).  Pixels outside the image
+ * read as 0, as divide_image's zero-initialised tiles do (JPEG.c:512-523).
+ *
+ * No torch types; device pointers are plain `void *` from hipMalloc (or a
+ * torch tensor's data_ptr()), `stream` is a hipStream_t (NULL = default).
+ * All functions return JPEGR_OK (0) or a negative JPEGR_ERR_* code.
+ */
+#ifndef JPEGR_H
+#define JPEGR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JPEGR_OK 0
+#define JPEGR_ERR_ARG (-1)     /* bad dimensions / NULL pointer */
+#define JPEGR_ERR_HIP (-2)     /* HIP runtime error (no GPU, launch failure) */
+#define JPEGR_ERR_NOMEM (-3)   /* device allocation failed */
+
+/* Number of int16 coefficients one w x h image produces: tiles * 128. */
+size_t jpegr_coef_count(int w, int h);
+
+/* Device API, asynchronous on `stream`.  `nimg` images of identical size,
+ * contiguous (image i at d_rgba + i*w*h*4, output at d_out + i*coef_count). */
+int jpegr_encode_device(const void *d_rgba, int w, int h, int nimg,
+                        void *d_out_i16, void *stream);
+
+/* Same tiles, but the un-quantised fp64 DCT coefficients in row-major
+ * (u*W+v) order per plane: [Y 64][Cr 32][Cb 32] doubles per tile.  This is
+ * the value discrete_cosine_transform (JPEG.c:451) leaves in *coefficients;
+ * exposed for bit-exact parity checks. */
+int jpegr_dct_raw_device(const void *d_rgba, int w, int h, int nimg,
+                         void *d_out_f64, void *stream);
+
+/* Host convenience: copies in, runs on the current device, copies out,
+ * synchronises.  `out` holds jpegr_coef_count(w, h) int16. */
+int jpegr_encode(const uint8_t *rgba, int w, int h, int16_t *out);
+
+/* Event-timed device run for measurement: runs jpegr_encode_device `iters`
+ * times on `stream` bracketed by HIP events recorded on that same stream and
+ * returns the mean milliseconds per launch in *ms_per_launch. */
+int jpegr_time_device(const void *d_rgba, int w, int h, int nimg,
+                      void *d_out_i16, int iters, void *stream,
+                      float *ms_per_launch);
+
+const char *jpegr_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JPEGR_H */

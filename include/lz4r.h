@@ -1,0 +1,110 @@
+/*
+ * lz4r.h -- C ABI of the MI355X "LZ4" compressor: the reference's exhaustive
+ * per-300-byte-block longest-match finder, greedy parser and custom
+ * token/sequence byte emitter, bit-exact to Algorithms/sequential/LZ4/LZ4.c
+ * (canonical semantics: matches are clamped at the block end).
+ *
+ * Entry points and the reference interface each replaces
+ * (Algorithms/sequential/LZ4/LZ4.c):
+ *   lz4r_compress_device / lz4r_compress   <- lz4_encode()            :670-742
+ *        (divide_input :123-177, the block loop :707-721, write_output
+ *         :427-441 minus the fixed file paths; the bytes written equal
+ *         compressed.bin)
+ *   per block inside the kernels            <- block_encode()          :506-620
+ *                                              find_longest_match()    :290-323
+ *                                              add_sequence_to_block() :443-459
+ *                                              write_sequence/_block() :365-425
+ *   lz4r_compress_segment_device            <- the same, for a run of whole
+ *        blocks without the frame header byte (multi-GPU shards)
+ *
+ * Stream format (frame := u8 nblocks&0xFF, block*; block := u8 nseq&0xFF,
+ * u16le (sum of sequence sizes + 3), sequence*).
+ *
+ * Errors: negative LZ4R_ERR_* codes instead of the reference's
+ * perror()+exit(1).  An input shorter than one block (300 B) is
+ * LZ4R_ERR_TOO_SMALL, the reference's exit(1) at LZ4.c:632-637.
+ *
+ * No torch types: device pointers are plain `void *`, `stream` is a
+ * hipStream_t passed as `void *` (NULL = legacy default stream).  A context
+ * owns the scratch buffers; one context per thread (or serialise).
+ */
+#ifndef LZ4R_H
+#define LZ4R_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LZ4R_BLOCK 300            /* DEFAULT_BLOCK_LENGTH, LZ4.c:23 */
+#define LZ4R_BLOCK_BOUND 1152     /* max encoded bytes of one block */
+
+#define LZ4R_OK 0
+#define LZ4R_ERR_ARG (-1)         /* NULL pointer / bad argument */
+#define LZ4R_ERR_TOO_SMALL (-2)   /* input < LZ4R_BLOCK (LZ4.c:632) */
+#define LZ4R_ERR_CAPACITY (-3)    /* output buffer too small; *out_len = need */
+#define LZ4R_ERR_HIP (-4)         /* HIP runtime error */
+#define LZ4R_ERR_NOMEM (-5)       /* device allocation failed */
+#define LZ4R_ERR_CORRUPT (-6)     /* decoder: malformed stream */
+
+typedef struct lz4r_ctx lz4r_ctx;
+
+/* Create a context bound to the current HIP device. */
+int lz4r_ctx_create(lz4r_ctx **ctx);
+void lz4r_ctx_destroy(lz4r_ctx *ctx);
+
+/* Worst-case compressed size of n input bytes (frame header included). */
+size_t lz4r_compress_bound(size_t n);
+size_t lz4r_nblocks(size_t n);
+
+/* Compress n bytes at d_in (device) into d_out (device, cap bytes) on
+ * `stream`, then synchronise it and return the compressed length in
+ * *out_len.  Frame header included.  Bytes equal lz4_encode()'s
+ * compressed.bin for the same input. */
+int lz4r_compress_device(lz4r_ctx *ctx, const void *d_in, size_t n,
+                         void *d_out, size_t cap, size_t *out_len,
+                         void *stream);
+
+/* Asynchronous form: enqueue only.  The compressed length (or the required
+ * capacity, if larger than cap: nothing past cap is written) is stored as a
+ * uint64 at d_out_len (device) when the stream reaches it. */
+int lz4r_compress_async(lz4r_ctx *ctx, const void *d_in, size_t n,
+                        void *d_out, size_t cap, void *d_out_len,
+                        void *stream);
+
+/* A run of whole 300-byte blocks (n need not be a multiple of 300 only for
+ * the globally last shard) without the frame header byte, for shards of a
+ * multi-GPU job; asynchronous, length at d_out_len like lz4r_compress_async.
+ * Concatenating the segments of consecutive shards after one header byte
+ * (u8 total_blocks & 0xFF) yields the single-GPU stream. */
+int lz4r_compress_segment_async(lz4r_ctx *ctx, const void *d_in, size_t n,
+                                void *d_out, size_t cap, void *d_out_len,
+                                void *stream);
+
+/* After a compress call: copy the first `count` per-block output offsets
+ * (uint64, exclusive scan, relative to the first block byte -- add 1 for a
+ * framed stream) of the last call to `dst` (host or device memory), then
+ * synchronise `stream`.  Used for sampled per-block parity checks at full
+ * size. */
+int lz4r_copy_block_offsets(const lz4r_ctx *ctx, void *dst, size_t count,
+                            void *stream);
+
+/* Host convenience wrapper around lz4r_compress_device (copies in and out). */
+int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
+                  size_t *out_len);
+
+/* Measurement: when enabled, every compress call records HIP events on its
+ * own launch stream around the whole call and around the match-finder/parse
+ * kernel (lz4_analyze, the dominant kernel).  lz4r_last_timing waits for the
+ * last call's end event and returns both durations in milliseconds. */
+int lz4r_set_timing(lz4r_ctx *ctx, int enable);
+int lz4r_last_timing(lz4r_ctx *ctx, float *ms_call, float *ms_match);
+
+const char *lz4r_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LZ4R_H */

@@ -1,0 +1,321 @@
+// jpegr.hip -- MI355X (gfx950) JPEG hot path: fused RGBA -> Y/Cr/Cb ->
+// 4:2:2 odd-column subsample -> 8x8 / 8x4 tiles -> fp64 DCT-II -> truncating
+// quantisation -> zigzag -> int16, one workgroup per 32-tile strip.
+//
+// Bit-exactness to Algorithms/sequential/JPEG/JPEG.c (x86-64, strict IEEE
+// double) rests on: fp64 throughout, no contraction (built with
+// -ffp-contract=off and the pragma below), the reference's summation order
+// (x outer, y inner, JPEG.c:477-485), the reference's product association
+// ((cv*cos_x)*cos_y, JPEG.c:483; (alpha_u*alpha_v)*sum, JPEG.c:489),
+// correctly-rounded fp64 division (JPEG.c:626) and the exact cos/alpha
+// values baked by gen_jpeg_tables.py.  No MFMA (fused multiply-add would
+// change the rounding) and no butterfly factorisation (changes the sum).
+//
+// Work split (per workgroup of 256 threads = 4 waves, 32 tiles of one tile
+// row):
+//   phase 1  every thread converts 8 pixels (2 x 16-B loads, coalesced 1 KiB
+//            rows) into centred doubles in LDS: Y tiles [32][64], Cr/Cb [32][32]
+//   phase 2  thread = (tile, u): Y row u, all 8 v  (64 products c*C8[x][u]
+//            shared by the 8 outputs: 2.125 fp64 ops per term, exact order)
+//   phase 3  thread = (tile, u): Cr and Cb row u, 4 v each
+//   phase 4  the strip's 32 x 256 B of int16 leave as coalesced 16-B stores.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "jpeg_tables.h"
+#include "../../include/jpegr.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kTiles = 32;       // tiles per workgroup strip
+constexpr int kThreads = 256;    // 4 waves
+constexpr int kYStride = 66;     // doubles per Y tile in LDS (528 B: bank skew 4)
+constexpr int kCStride = 34;     // doubles per chroma tile (272 B: bank skew 4)
+
+__constant__ double dC8[8][8];
+__constant__ double dAA88[8][8];
+__constant__ double dAA84[8][4];
+__constant__ int dLQ[64];
+__constant__ int dCQ[32];
+__constant__ int dZZ8[64];
+__constant__ int dZZ4[32];
+
+__device__ __forceinline__ int clamp_u8(int v) {       // JPEG.c:132-139
+  return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// One pixel's contribution to the tile planes (JPEG.c:127, 157, 180;
+// chroma only from odd columns: chroma_subsample JPEG.c:329-331 +
+// divide_image JPEG.c:540-544).  `valid` = inside the image.
+__device__ __forceinline__ void convert_pixel(uint32_t p, bool valid, int r,
+                                              int px, double *ylds,
+                                              double *crl, double *cbl) {
+  const int tile = px >> 3, col = px & 7;
+  const unsigned R = p & 255u, G = (p >> 8) & 255u, B = (p >> 16) & 255u;
+  int yv = 0;
+  if (valid) {
+    double y = 0.299 * (double)R + 0.587 * (double)G + 0.114 * (double)B;
+    yv = (int)(uint8_t)(unsigned)y;            // (uint8_t) of a double in [0,256)
+  }
+  ylds[tile * kYStride + r * 8 + col] = (double)(yv - 128);   // JPEG.c:467
+  if (col & 1) {
+    int crv = 0, cbv = 0;
+    if (valid) {
+      crv = clamp_u8((int)(0.439 * (double)R - 0.368 * (double)G -
+                           0.071 * (double)B + 128.0));
+      cbv = clamp_u8((int)(-0.148 * (double)R - 0.291 * (double)G +
+                           0.439 * (double)B + 128.0));
+    }
+    const int ci = tile * kCStride + r * 4 + (col >> 1);
+    crl[ci] = (double)(crv - 128);
+    cbl[ci] = (double)(cbv - 128);
+  }
+}
+
+template <bool RAW>
+__global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
+    const uint8_t *__restrict__ rgba, int w, int h, int tiles_x, int tiles_y,
+    int strips, void *__restrict__ out) {
+  __shared__ double ylds[kTiles * kYStride];
+  __shared__ double crl[kTiles * kCStride];
+  __shared__ double cbl[kTiles * kCStride];
+  __shared__ __attribute__((aligned(16))) int16_t olds[RAW ? 8 : kTiles * 128];
+
+  const int img = blockIdx.y;
+  const int br = blockIdx.x / strips;
+  const int bc0 = (blockIdx.x - br * strips) * kTiles;
+  const int ntiles = min(kTiles, tiles_x - bc0);
+  const size_t img_px = (size_t)w * (size_t)h;
+  const uint8_t *src = rgba + (size_t)img * img_px * 4;
+  const int t = threadIdx.x;
+
+  // ---- phase 1: colour conversion into LDS --------------------------------
+  {
+    const int r = t >> 5;           // tile row 0..7
+    const int c = t & 31;
+    const int row = br * 8 + r;
+    const bool row_ok = row < h;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int lx = half * 128 + c * 4;   // pixel column within the strip
+      const int x = bc0 * 8 + lx;
+      uint32_t p[4];
+      bool ok[4];
+      if (row_ok && ((w & 3) == 0) && x + 3 < w) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(
+            src + ((size_t)row * w + x) * 4);
+        p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w;
+        ok[0] = ok[1] = ok[2] = ok[3] = true;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          ok[k] = row_ok && (x + k < w);
+          p[k] = 0;
+          if (ok[k]) {
+            const uint8_t *q = src + ((size_t)row * w + x + k) * 4;
+            p[k] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) convert_pixel(p[k], ok[k], r, lx + k, ylds, crl, cbl);
+    }
+  }
+  __syncthreads();
+
+  const int tile = t >> 3;   // 0..31
+  const int u = t & 7;
+  const size_t tile_g = ((size_t)img * tiles_y + br) * tiles_x + bc0 + tile;
+  const bool tile_ok = tile < ntiles;
+
+  double cx[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) cx[x] = dC8[x][u];
+
+  // ---- phase 2: luma DCT row u (JPEG.c:471-491 with W=H=8) -----------------
+  {
+    const double *yt = ylds + tile * kYStride;
+    double s[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) s[v] = 0.0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+#pragma unroll
+      for (int y = 0; y < 8; ++y) {
+        const double tv = yt[x * 8 + y] * cx[x];                 // cv*cos_x
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+          s[v] = s[v] + tv * jpegr_tables::C8[y][v];             // *cos_y, +=
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const double coef = dAA88[u][v] * s[v];                    // JPEG.c:489
+      if (RAW) {
+        if (tile_ok) static_cast<double *>(out)[tile_g * 128 + u * 8 + v] = coef;
+      } else {
+        const int q = (int)(coef / (double)dLQ[u * 8 + v]);      // JPEG.c:626-627
+        olds[tile * 128 + dZZ8[u * 8 + v]] = (int16_t)q;
+      }
+    }
+  }
+
+  // ---- phase 3: chroma DCTs row u (JPEG.c:1139-1140: width 4, height 8) ----
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    const double *ct = (ch == 0 ? crl : cbl) + tile * kCStride;
+    double s[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) s[v] = 0.0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const double tv = ct[x * 4 + y] * cx[x];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) s[v] = s[v] + tv * jpegr_tables::C4[y][v];
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const double coef = dAA84[u][v] * s[v];
+      if (RAW) {
+        if (tile_ok)
+          static_cast<double *>(out)[tile_g * 128 + 64 + ch * 32 + u * 4 + v] = coef;
+      } else {
+        const int q = (int)(coef / (double)dCQ[u * 4 + v]);
+        olds[tile * 128 + 64 + ch * 32 + dZZ4[u * 4 + v]] = (int16_t)q;
+      }
+    }
+  }
+
+  if (RAW) return;
+  __syncthreads();
+
+  // ---- phase 4: coalesced store of the strip's tiles -------------------------
+  {
+    uint8_t *dst = static_cast<uint8_t *>(out) +
+                   (((size_t)img * tiles_y + br) * tiles_x + bc0) * 256;
+    const int bytes = ntiles * 256;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int off = (k * kThreads + t) * 16;
+      if (off < bytes)
+        *reinterpret_cast<uint4 *>(dst + off) =
+            *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(olds) + off);
+    }
+  }
+}
+
+bool g_tables_ready[64] = {false};
+
+hipError_t upload_tables() {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev >= 0 && dev < 64 && g_tables_ready[dev]) return hipSuccess;
+  using namespace jpegr_tables;
+  int lq[64], cq[32], z8[64], z4[32];
+  for (int i = 0; i < 64; ++i) { lq[i] = LUMA_Q[i]; z8[i] = ZZ8_POS[i]; }
+  for (int i = 0; i < 32; ++i) { cq[i] = CHROMA_Q[i]; z4[i] = ZZ4_POS[i]; }
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dC8), C8, sizeof(C8))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dAA88), AA88, sizeof(AA88))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dAA84), AA84, sizeof(AA84))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dLQ), lq, sizeof(lq))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dCQ), cq, sizeof(cq))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ8), z8, sizeof(z8))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ4), z4, sizeof(z4))) != hipSuccess) return e;
+  if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
+  return hipSuccess;
+}
+
+int launch(bool raw, const void *d_rgba, int w, int h, int nimg, void *d_out,
+           void *stream) {
+  if (!d_rgba || !d_out || w <= 0 || h <= 0 || nimg <= 0 || nimg > 65535)
+    return JPEGR_ERR_ARG;
+  if (upload_tables() != hipSuccess) return JPEGR_ERR_HIP;
+  const int tx = (w + 7) / 8, ty = (h + 7) / 8;
+  const int strips = (tx + kTiles - 1) / kTiles;
+  const long long gx = (long long)ty * strips;
+  if (gx > 0x7fffffffLL) return JPEGR_ERR_ARG;
+  dim3 grid((unsigned)gx, (unsigned)nimg);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (raw)
+    hipLaunchKernelGGL(jpeg_strip_kernel<true>, grid, dim3(kThreads), 0, s,
+                       static_cast<const uint8_t *>(d_rgba), w, h, tx, ty, strips, d_out);
+  else
+    hipLaunchKernelGGL(jpeg_strip_kernel<false>, grid, dim3(kThreads), 0, s,
+                       static_cast<const uint8_t *>(d_rgba), w, h, tx, ty, strips, d_out);
+  return hipGetLastError() == hipSuccess ? JPEGR_OK : JPEGR_ERR_HIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t jpegr_coef_count(int w, int h) {
+  if (w <= 0 || h <= 0) return 0;
+  return (size_t)((w + 7) / 8) * (size_t)((h + 7) / 8) * 128;
+}
+
+int jpegr_encode_device(const void *d_rgba, int w, int h, int nimg, void *d_out,
+                        void *stream) {
+  return launch(false, d_rgba, w, h, nimg, d_out, stream);
+}
+
+int jpegr_dct_raw_device(const void *d_rgba, int w, int h, int nimg,
+                         void *d_out, void *stream) {
+  return launch(true, d_rgba, w, h, nimg, d_out, stream);
+}
+
+int jpegr_encode(const uint8_t *rgba, int w, int h, int16_t *out) {
+  if (!rgba || !out || w <= 0 || h <= 0) return JPEGR_ERR_ARG;
+  const size_t in_b = (size_t)w * h * 4, out_b = jpegr_coef_count(w, h) * 2;
+  void *din = nullptr, *dout = nullptr;
+  if (hipMalloc(&din, in_b) != hipSuccess) return JPEGR_ERR_NOMEM;
+  if (hipMalloc(&dout, out_b) != hipSuccess) { (void)hipFree(din); return JPEGR_ERR_NOMEM; }
+  int rc = JPEGR_OK;
+  if (hipMemcpy(din, rgba, in_b, hipMemcpyHostToDevice) != hipSuccess) rc = JPEGR_ERR_HIP;
+  if (rc == JPEGR_OK) rc = jpegr_encode_device(din, w, h, 1, dout, nullptr);
+  if (rc == JPEGR_OK && hipMemcpy(out, dout, out_b, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = JPEGR_ERR_HIP;
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  return rc;
+}
+
+int jpegr_time_device(const void *d_rgba, int w, int h, int nimg, void *d_out,
+                      int iters, void *stream, float *ms_per_launch) {
+  if (iters <= 0 || !ms_per_launch) return JPEGR_ERR_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipEvent_t a, b;
+  if (hipEventCreate(&a) != hipSuccess) return JPEGR_ERR_HIP;
+  if (hipEventCreate(&b) != hipSuccess) { (void)hipEventDestroy(a); return JPEGR_ERR_HIP; }
+  int rc = JPEGR_OK;
+  (void)hipEventRecord(a, s);
+  for (int i = 0; i < iters && rc == JPEGR_OK; ++i)
+    rc = jpegr_encode_device(d_rgba, w, h, nimg, d_out, stream);
+  (void)hipEventRecord(b, s);
+  if (hipEventSynchronize(b) != hipSuccess) rc = JPEGR_ERR_HIP;
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, a, b);
+  *ms_per_launch = ms / iters;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return rc;
+}
+
+const char *jpegr_strerror(int code) {
+  switch (code) {
+    case JPEGR_OK: return "ok";
+    case JPEGR_ERR_ARG: return "invalid argument";
+    case JPEGR_ERR_HIP: return "HIP runtime error";
+    case JPEGR_ERR_NOMEM: return "device allocation failed";
+    default: return "unknown error";
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,103 @@
+"""Multi-GPU sharding of the LZ4 path: one process per GPU, static split of
+whole 300-byte blocks, one exchange (RCCL over xGMI with backend "nccl";
+gloo on CPU for tests).
+
+Blocks are independent (the match window is the block prefix: p < 300 <
+WINDOW_SIZE, LZ4.c:295), so rank r compresses blocks [b0, b1) with no data-path
+communication -- the reference's thread-per-block decomposition
+(Algorithms/parallel/LZ4/LZ4.c:742) lifted to GPUs.  The only collective is the
+assembly of the framed stream:
+  1. all_gather of one int64 segment length per rank -> exclusive offsets
+     (every rank then knows where its segment lands in the global stream);
+  2. gatherv of the segments to the destination rank as batched P2P
+     send/recv (segment sizes differ, so no padded gather), which writes the
+     frame header byte u8(total_blocks) in front (write_output, LZ4.c:429).
+Concatenation is exact because a block's bytes depend only on that block.
+
+The JPEG path shards images (or tile rows) with no exchange at all.
+"""
+import torch
+import torch.distributed as dist
+
+BLOCK = 300
+
+
+def nblocks(n):
+    return (n + BLOCK - 1) // BLOCK
+
+
+def shard_blocks(nb, world, rank):
+    """Contiguous, balanced range of whole blocks [b0, b1) for `rank`."""
+    return (nb * rank) // world, (nb * (rank + 1)) // world
+
+
+def shard_bytes(n, world, rank):
+    """Byte range [lo, hi) of rank's shard of an n-byte input: block aligned,
+    only the globally last shard may end in a short block."""
+    b0, b1 = shard_blocks(nblocks(n), world, rank)
+    return b0 * BLOCK, min(b1 * BLOCK, n)
+
+
+def exchange_lengths(seg_len, device, group=None):
+    """all_gather of every rank's segment length -> (lengths list, offsets list)."""
+    world = dist.get_world_size(group)
+    mine = torch.tensor([seg_len], dtype=torch.int64, device=device)
+    allv = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(allv, mine, group=group)
+    lens = [int(x) for x in allv.cpu().tolist()]
+    offs, acc = [], 0
+    for L in lens:
+        offs.append(acc)
+        acc += L
+    return lens, offs
+
+
+def gather_stream(segment, seg_len, nb_total, lens, offs, dst=0, group=None):
+    """Assemble [u8 nb_total] + seg_0 + ... + seg_{W-1} on rank `dst`.
+    `segment` is this rank's uint8 tensor (at least seg_len bytes) on the
+    backend's device.  Returns the framed stream tensor on dst, None elsewhere."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    if rank == dst:
+        total = 1 + sum(lens)
+        out = torch.empty(total, dtype=torch.uint8, device=segment.device)
+        out[0] = nb_total & 0xFF
+        out[1 + offs[rank]:1 + offs[rank] + seg_len].copy_(segment[:seg_len])
+        ops = []
+        for r in range(world):
+            if r == dst or lens[r] == 0:
+                continue
+            view = out[1 + offs[r]:1 + offs[r] + lens[r]]
+            ops.append(dist.P2POp(dist.irecv, view, r, group=group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return out
+    if seg_len > 0:
+        op = dist.P2POp(dist.isend, segment[:seg_len].contiguous(), dst, group=group)
+        for req in dist.batch_isend_irecv([op]):
+            req.wait()
+    return None
+
+
+def compress_sharded(local, n_total, compress_segment, dst=0, group=None):
+    """Full sharded job on this rank's slice `local` (uint8 tensor of
+    shard_bytes(n_total, W, rank)).  `compress_segment(tensor) -> (out, len)`
+    is the per-rank compressor (the HIP path in production; tests may pass a
+    CPU checker).  Returns the framed stream on dst, None elsewhere."""
+    seg, seg_len = compress_segment(local)
+    lens, offs = exchange_lengths(seg_len, seg.device, group)
+    return gather_stream(seg, seg_len, nblocks(n_total), lens, offs, dst, group)
+
+
+def hip_segment_compressor(compressor, stream=None):
+    """compress_segment callable over the HIP path (lz4r_compress_segment_async)."""
+    from .lz4 import compress_bound
+
+    def run(local):
+        n = local.numel()
+        out = torch.empty(compress_bound(n), dtype=torch.uint8, device=local.device)
+        d_len = torch.zeros(1, dtype=torch.int64, device=local.device)
+        compressor.compress_async(local, n, out, d_len, stream=stream, segment=True)
+        return out, int(d_len.item())
+    return run

@@ -1,0 +1,144 @@
+"""Host-side mirror of the reference's LZ4 encoder interface over the HIP path.
+
+Reference (Algorithms/sequential/LZ4/LZ4.c):
+  lz4_encode()         :670-742  file in -> compressed.bin  ==  compress(bytes)
+  divide_input()       :123-177  300-byte blocks            ==  nblocks()/shard_blocks()
+  block_encode() + find_longest_match()  run inside the HIP kernels.
+
+Errors follow the reference's exit paths as exceptions: an input shorter than
+300 bytes raises InputTooSmall (the reference prints and exit(1)s, :632-637).
+Device memory and streams come from torch (plumbing only); the compute is the
+C ABI in include/lz4r.h.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import Lz4Error, LZ4R_BLOCK, LZ4R_BLOCK_BOUND
+
+BLOCK = LZ4R_BLOCK
+
+
+class InputTooSmall(Lz4Error):
+    pass
+
+
+def _raise(code, where):
+    if code == _lib.LZ4R_ERR_TOO_SMALL:
+        raise InputTooSmall(code, where)
+    raise Lz4Error(code, where)
+
+
+def nblocks(n):
+    return (n + BLOCK - 1) // BLOCK
+
+
+def compress_bound(n):
+    return int(_lib.lib().lz4r_compress_bound(n))
+
+
+def _stream_handle(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class Compressor:
+    """Owns an lz4r context (device scratch) on the current device."""
+
+    def __init__(self):
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        rc = L.lz4r_ctx_create(ctypes.byref(h))
+        if rc != 0:
+            _raise(rc, "lz4r_ctx_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().lz4r_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- device API -------------------------------------------------------
+    def compress_device(self, d_in, n=None, d_out=None, stream=None):
+        """Compress the uint8 CUDA tensor d_in (first n bytes).  Returns
+        (d_out, length): the framed stream is d_out[:length]."""
+        import torch
+        n = d_in.numel() if n is None else n
+        if d_out is None:
+            d_out = torch.empty(compress_bound(n), dtype=torch.uint8, device=d_in.device)
+        got = ctypes.c_size_t(0)
+        rc = _lib.lib().lz4r_compress_device(self._h, ctypes.c_void_p(d_in.data_ptr()), n,
+                                             ctypes.c_void_p(d_out.data_ptr()), d_out.numel(),
+                                             ctypes.byref(got), _stream_handle(stream))
+        if rc != 0:
+            _raise(rc, "lz4r_compress_device")
+        return d_out, got.value
+
+    def compress_async(self, d_in, n, d_out, d_len, stream=None, segment=False):
+        """Enqueue only; the uint64 length lands in d_len (1-element int64 tensor).
+        segment=True: whole blocks without the frame header (one shard)."""
+        fn = (_lib.lib().lz4r_compress_segment_async if segment
+              else _lib.lib().lz4r_compress_async)
+        rc = fn(self._h, ctypes.c_void_p(d_in.data_ptr()), n, ctypes.c_void_p(d_out.data_ptr()),
+                d_out.numel(), ctypes.c_void_p(d_len.data_ptr()), _stream_handle(stream))
+        if rc != 0:
+            _raise(rc, "lz4r_compress_async")
+
+    def block_offsets(self, count, stream=None):
+        """numpy uint64 array: the last call's first `count` per-block output
+        offsets (relative to the first block byte)."""
+        out = np.empty(count, dtype=np.uint64)
+        rc = _lib.lib().lz4r_copy_block_offsets(self._h, out.ctypes.data_as(ctypes.c_void_p),
+                                                count, _stream_handle(stream))
+        if rc != 0:
+            _raise(rc, "lz4r_copy_block_offsets")
+        return out
+
+    def set_timing(self, enable=True):
+        """Record HIP events on the launch stream around each call and its
+        match-finder/parse kernel (see last_timing)."""
+        _lib.lib().lz4r_set_timing(self._h, 1 if enable else 0)
+
+    def last_timing(self):
+        """(ms of the whole last call, ms of its lz4_analyze kernel)."""
+        a, b = ctypes.c_float(0), ctypes.c_float(0)
+        rc = _lib.lib().lz4r_last_timing(self._h, ctypes.byref(a), ctypes.byref(b))
+        if rc != 0:
+            _raise(rc, "lz4r_last_timing")
+        return a.value, b.value
+
+    # -- host convenience -------------------------------------------------
+    def compress(self, data):
+        """bytes -> framed compressed bytes (== the reference's compressed.bin)."""
+        import torch
+        buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        if buf.size < BLOCK:
+            raise InputTooSmall(_lib.LZ4R_ERR_TOO_SMALL, "compress")
+        d_in = torch.from_numpy(buf.copy()).cuda()
+        d_out, length = self.compress_device(d_in)
+        torch.cuda.synchronize()
+        return d_out[:length].cpu().numpy().tobytes()
+
+
+def compress(data):
+    """One-shot host API: compressed bytes of `data` (a bytes-like object)."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8)
+    n = buf.size
+    if n < BLOCK:
+        raise InputTooSmall(_lib.LZ4R_ERR_TOO_SMALL, "lz4r_compress")
+    cap = 1 + nblocks(n) * LZ4R_BLOCK_BOUND
+    out = np.empty(cap, dtype=np.uint8)
+    got = ctypes.c_size_t(0)
+    rc = _lib.lib().lz4r_compress(buf.ctypes.data_as(ctypes.c_void_p), n,
+                                  out.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(got))
+    if rc != 0:
+        _raise(rc, "lz4r_compress")
+    return out[:got.value].tobytes()

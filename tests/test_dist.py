@@ -1,0 +1,82 @@
+"""The N>1 path on CPU: gloo, world_size 2 (and 3), static whole-block shards,
+length all_gather + P2P gatherv.  The per-rank compressor here is the CPU
+oracle (a test checker standing in for the GPU); on the GPU box the same
+dist.compress_sharded runs with lz4jpeg.dist.hip_segment_compressor."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from lz4jpeg import dist as ldist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, data, expect, q):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "lz4-jpeg_amd"))
+    import oracle_api
+    from lz4jpeg import dist as d
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        o = oracle_api.load()
+        n = len(data)
+        lo, hi = d.shard_bytes(n, world, rank)
+        local = torch.from_numpy(np.frombuffer(data[lo:hi], dtype=np.uint8).copy())
+
+        def seg(t):
+            b = t.numpy()
+            nb = (b.size + 299) // 300
+            out = o.lz4_blocks(b, 0, nb)
+            return torch.from_numpy(np.frombuffer(out, dtype=np.uint8).copy()), len(out)
+
+        got = d.compress_sharded(local, n, seg, dst=0)
+        if rank == 0:
+            q.put(bytes(got.numpy().tobytes()) == expect)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 300 * 41 + 17), (2, 300 * 40), (3, 300 * 7 + 1),
+                                     (2, 300 * 3)])
+def test_sharded_stream_equals_single(oracle, world, n):
+    import golden_inputs
+    data = golden_inputs.lz4_input("metamorphosis_spaces")[:n]
+    expect = oracle.lz4_compress(data)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, expect, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert q.get(timeout=5) is True
+
+
+def test_shards_are_block_aligned_and_cover():
+    for n in [300, 301, 12345, 10 ** 6 + 7, 1 << 30]:
+        for world in [1, 2, 3, 4, 8]:
+            prev = 0
+            for r in range(world):
+                lo, hi = ldist.shard_bytes(n, world, r)
+                assert lo == prev and lo % 300 == 0
+                assert hi == n or hi % 300 == 0
+                prev = hi
+            assert prev == n

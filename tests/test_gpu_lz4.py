@@ -1,0 +1,151 @@
+"""HIP LZ4 path vs the pinned CPU oracle: bit-exact on golden vectors, edge
+cases and seeded fuzz; at BASELINE.json's full size (1 GiB) by sampled
+per-block parity and a decode round trip.  All calls go through the C ABI."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import golden_inputs
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(golden_inputs.GOLDEN, "golden.json")))
+
+
+@pytest.fixture(scope="module")
+def comp(gpu):
+    from lz4jpeg.lz4 import Compressor
+    c = Compressor()
+    yield c
+    c.close()
+
+
+def _gpu_compress(comp, data):
+    import torch
+    d_in = torch.from_numpy(np.frombuffer(bytes(data), dtype=np.uint8).copy()).cuda()
+    d_out, n = comp.compress_device(d_in)
+    torch.cuda.synchronize()
+    return d_out[:n].cpu().numpy().tobytes()
+
+
+@pytest.mark.parametrize("e", GOLDEN["lz4"], ids=lambda e: e["name"])
+def test_golden(comp, e):
+    data = golden_inputs.lz4_input(e["input"])
+    got = _gpu_compress(comp, data)
+    assert len(got) == e["out_len"]
+    assert hashlib.md5(got).hexdigest() == e["md5"]
+
+
+def test_committed_compressed_bin(comp):
+    data = golden_inputs.lz4_input("file:lz4_input.txt")
+    ref = open(os.path.join(golden_inputs.GOLDEN, "lz4_input.compressed.bin"), "rb").read()
+    assert _gpu_compress(comp, data) == ref
+
+
+def test_host_api_matches(comp, oracle):
+    from lz4jpeg import lz4
+    data = golden_inputs.lz4_input("text_10000")
+    assert lz4.compress(data) == oracle.lz4_compress(data)
+    assert comp.compress(data) == oracle.lz4_compress(data)
+
+
+def test_too_small_raises(comp):
+    from lz4jpeg import lz4
+    with pytest.raises(lz4.InputTooSmall):
+        lz4.compress(b"x" * 299)
+
+
+def _fuzz_inputs():
+    rng = np.random.default_rng(1234)
+    text = golden_inputs.lz4_input("metamorphosis_spaces")
+    cases = []
+    for k in range(40):
+        n = int(rng.integers(300, 40_000))
+        kind = k % 5
+        if kind == 0:
+            s = int(rng.integers(0, len(text) - n))
+            b = text[s:s + n]
+        elif kind == 1:
+            b = rng.integers(0, int(rng.integers(2, 8)), n, dtype=np.uint8).tobytes()
+        elif kind == 2:
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif kind == 3:  # repeated short motifs with noise
+            motif = rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8)
+            b = np.resize(motif, n)
+            flips = rng.integers(0, n, n // 50)
+            b[flips] = rng.integers(0, 256, flips.size, dtype=np.uint8)
+            b = b.tobytes()
+        else:  # runs of one byte of random lengths (uint8 truncation region)
+            out = bytearray()
+            while len(out) < n:
+                out += bytes([int(rng.integers(0, 4))]) * int(rng.integers(1, 400))
+            b = bytes(out[:n])
+        cases.append(b)
+    return cases
+
+
+@pytest.mark.parametrize("idx", range(40))
+def test_fuzz_vs_oracle(comp, oracle, idx):
+    data = _fuzz_inputs()[idx]
+    assert _gpu_compress(comp, data) == oracle.lz4_compress(data)
+
+
+def test_segments_concatenate_to_stream(comp, oracle):
+    """Shard outputs (lz4r_compress_segment_async) + header byte == framed stream."""
+    import torch
+    from lz4jpeg import dist as ldist
+    data = golden_inputs.lz4_input("metamorphosis_spaces")
+    n = len(data)
+    nb = ldist.nblocks(n)
+    parts = []
+    for r in range(3):
+        lo, hi = ldist.shard_bytes(n, 3, r)
+        d_in = torch.from_numpy(np.frombuffer(data[lo:hi], dtype=np.uint8).copy()).cuda()
+        out = torch.empty(1 + ldist.nblocks(hi - lo) * 1152, dtype=torch.uint8, device="cuda")
+        d_len = torch.zeros(1, dtype=torch.int64, device="cuda")
+        comp.compress_async(d_in, hi - lo, out, d_len, segment=True)
+        torch.cuda.synchronize()
+        parts.append(out[:int(d_len.item())].cpu().numpy().tobytes())
+    assert bytes([nb & 0xFF]) + b"".join(parts) == oracle.lz4_compress(data)
+
+
+def test_capacity_error_reports_need(comp):
+    import torch
+    from lz4jpeg import lz4
+    data = golden_inputs.lz4_input("text_10000")
+    d_in = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    small = torch.zeros(100, dtype=torch.uint8, device="cuda")
+    with pytest.raises(lz4.Lz4Error) as ei:
+        comp.compress_device(d_in, d_out=small)
+    assert ei.value.code == -3
+    assert small.cpu().numpy().any()            # bytes up to cap were written
+
+
+@pytest.mark.slow
+def test_full_size_1gib_sampled_parity_and_roundtrip(comp, oracle):
+    """BASELINE.json config 2: 1 GiB random_extract-style text.  Every block's
+    bytes are checked for 4096 random blocks (+ first/last) against the oracle,
+    and the whole stream decodes back to the input."""
+    import torch
+    from lz4jpeg import synth
+    n = 1 << 30
+    data = synth.random_passages(n, length=30000, seed=1)
+    d_in = torch.from_numpy(data).cuda()
+    d_out, length = comp.compress_device(d_in)
+    torch.cuda.synchronize()
+    nb = (n + 299) // 300
+    offs = comp.block_offsets(nb)
+    stream = d_out[:length].cpu().numpy()
+    assert stream[0] == nb & 0xFF
+    rng = np.random.default_rng(7)
+    sample = np.unique(np.concatenate([[0, nb - 1], rng.integers(0, nb, 4096)]))
+    for b in sample:
+        lo = 1 + int(offs[b])
+        hi = 1 + int(offs[b + 1]) if b + 1 < nb else length
+        assert stream[lo:hi].tobytes() == oracle.lz4_blocks(data, int(b), int(b) + 1), b
+    dec = oracle.lz4_decompress(stream.tobytes(), nb, n + 300)
+    assert len(dec) == n
+    assert dec == data.tobytes()
