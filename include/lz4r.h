@@ -83,6 +83,13 @@ int lz4r_compress_segment_async(lz4r_ctx *ctx, const void *d_in, size_t n,
                                 void *d_out, size_t cap, void *d_out_len,
                                 void *stream);
 
+/* After a compress call: copy the encoded byte count (uint16) of each of the
+ * first `count` blocks of the last call to `dst` (host or device memory),
+ * then synchronise `stream`.  Block b's bytes start at sum(sizes[0..b)) after
+ * the frame header byte.  Written by the kernel on every call (2 B/block). */
+int lz4r_copy_block_sizes(const lz4r_ctx *ctx, void *dst, size_t count,
+                          void *stream);
+
 /* After a compress call: copy the first `count` per-block output offsets
  * (uint64, exclusive scan, relative to the first block byte -- add 1 for a
  * framed stream) of the last call to `dst` (host or device memory), then
@@ -96,8 +103,8 @@ int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
                   size_t *out_len);
 
 /* Measurement: when enabled, every compress call records HIP events on its
- * own launch stream around the whole call and around the match-finder/parse
- * kernel (lz4_analyze, the dominant kernel).  lz4r_last_timing waits for the
+ * own launch stream around the whole call and around the compressor kernel
+ * (lz4_tiles, the only kernel of the call).  lz4r_last_timing waits for the
  * last call's end event and returns both durations in milliseconds. */
 int lz4r_set_timing(lz4r_ctx *ctx, int enable);
 int lz4r_last_timing(lz4r_ctx *ctx, float *ms_call, float *ms_match);

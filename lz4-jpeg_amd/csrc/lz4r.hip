@@ -5,72 +5,120 @@
 // in every block, greedily parses with an exhaustive longest-match search over
 // the whole block prefix (find_longest_match, LZ4.c:290-323; strict '>' so the
 // smallest i -- farthest offset -- wins ties; length truncated to uint8_t).
-// Every block is independent, so the GPU decomposition is:
+// Blocks are independent, so the whole compressor is ONE single-pass kernel.
 //
-//   lz4_analyze  one wave per group of kG blocks staged in LDS.
-//     index (wave-parallel, per block): every position p <= n-4 gets its
-//       4-byte key; positions are chained into per-bucket circular lists
-//       (LDS hash table, atomic exchange); a lane per position walks its
-//       cycle to set has_match[p] (exists i < p with an equal key, i.e. a
-//       match of length >= 4).  Exact: any match >= 4 starts with an equal
-//       4-gram, every equal 4-gram is in the same bucket, and the result
-//       does not depend on the order the atomics ran in.
-//     parse (lane per block): greedy walk that jumps over literal runs with
-//       the has_match bitmask (find-first-set) and, at each candidate
-//       position, walks the cycle: lcp with every earlier equal-key position
-//       (4 bytes per compare), best = max length, ties -> smallest i.
-//       Emits one packed record per sequence (L | M<<9 | dist<<17) and the
-//       block's encoded byte count.
-//   lz4_scan_*   exclusive scan of per-block byte counts -> output offsets.
-//   lz4_emit     one wave per block: records -> token/size/ext/literals/
-//       offset bytes at the block's output offset (write_sequence,
-//       LZ4.c:365-413; write_block :415-425; frame byte :429).
+// lz4_tiles: persistent; workgroup = one wave; tiles of kTB = 8 consecutive
+// blocks (2,400 B) dealt round-robin to the resident waves.  Per tile:
+//   stage    tile bytes -> LDS (16-B loads: the only HBM read).
+//   per block, position-parallel (lane owns p = 64r + lane, r < 5):
+//     index  every 4-gram start p is chained into its LDS hash bucket
+//            (atomic exchange; the bucket lists are closed into cycles, so
+//            the result does not depend on atomic order).  A chain entry is
+//            self-describing: position | preceding byte | 15-bit hash tag.
+//     local  each lane walks its 5 cycles interleaved (one LDS read per
+//            step) and measures only LEFT-MAXIMAL candidates j < p (equal
+//            4-gram, and j == 0 or blk[j-1] != blk[p-1]): the longest one,
+//            ties to the smallest j, is local(p).
+//     best   a candidate that is not left-maximal is the pair (j-1, p-1)
+//            shifted by one, whose match is one byte longer.  Hence
+//              best(p) = lexmax over q <= p of (q + local_len(q), q - local_j(q))
+//            i.e. the longest match ends furthest right and, among equals,
+//            has the largest distance (= smallest source, LZ4.c:307).  One
+//            wave max-scan (DPP) over the positions gives best() for all p.
+//            M = len & 0xFF (the uint8_t return, LZ4.c:317).
+//     parse  nm(x) = first matchable position >= x (ballot masks);
+//            succ(c) = nm(c + M(c)); the greedy parse (LZ4.c:516-583) is the
+//            walk c0 = nm(0), c_{k+1} = succ(c_k), one LDS read per sequence.
+//     emit   sequence k on lane k: sizes, wave scan for offsets, token /
+//            size / literal-extension / offset bytes (write_sequence,
+//            LZ4.c:365-413), then a position-parallel literal scatter, into
+//            the tile's LDS output (overlaying already-consumed input).
+//   publish  decoupled look-back over tile byte counts (one 8-byte
+//            {epoch, flag, value} word per tile) -> tile's output offset.
+//   store    LDS -> HBM as aligned 16-B stores.
+// HBM traffic per input byte: 1 B read + ~1.03 B written (+2 B per block of
+// per-block sizes).  Forward progress of the look-back: every tile waits only
+// on lower tiles, each wave takes its tiles in increasing order and the grid
+// never exceeds the co-resident wave count (lz4r_ctx.max_grid).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <new>
+#include <vector>
 
 #include "../../include/lz4r.h"
 
+// LZ4R_VARIANT (timing ablations only, never shipped): 1 = no match search,
+// 2 = no index/match phase, 3 = 2 + no look-back (fixed output slots),
+// 4 = full search, no look-back
+#ifndef LZ4R_VARIANT
+#define LZ4R_VARIANT 0
+#endif
+
+#ifdef LZ4R_PROF
+__device__ unsigned long long g_prof[16];
+__device__ __forceinline__ uint64_t prof_now() {
+  uint64_t t;
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  return t;
+}
+#define PROF_T(i) do { const uint64_t _t = prof_now(); prof[i] += _t - prof_last; prof_last = _t; } while (0)
+#else
+#define PROF_T(i) do { } while (0)
+#endif
+
 namespace {
 
-constexpr int kBlk = LZ4R_BLOCK;   // 300
-constexpr int kG = 16;             // blocks per analyze wave
-constexpr int kH = 512;            // hash buckets of the per-block index
-constexpr int kHashShift = 32 - 9;
-constexpr int kMaxRec = 128;       // >= 75 (M>=4) + 44 (M in 1..3, q<=43) + 1
-constexpr uint32_t kEmpty = 0xFFFFFFFFu;
-constexpr int kChunkBytes = kG * kBlk;          // 4800, multiple of 16
-constexpr int kDataWords = (kChunkBytes + 16) / 4;
+constexpr int kBlk = LZ4R_BLOCK;          // 300
+constexpr int kTB = 8;                    // blocks per tile
+constexpr int kTileIn = kTB * kBlk;       // 2400 B, multiple of 16
+constexpr int kBlkOutMax = 600;           // >= 548: worst-case bytes of one block
+// The tile's output grows from buf[0]; block k's input sits at
+// kInOff + 300k.  Writing block k's bytes never reaches its own input:
+// (k+1)*kBlkOutMax <= kInOff + 300k for k < kTB.
+constexpr int kInOff = ((kTB * kBlkOutMax - (kTB - 1) * kBlk) + 15) / 16 * 16;
+constexpr int kRegion = kInOff + kTileIn + 48;  // + over-read pad (lcp, 32-B copy reads)
+constexpr int kHB = 9;                    // hash bits: 512 buckets
+constexpr int kH = 1 << kHB;
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;  // position field 511 = none
+constexpr int kArr = kBlk + 4;
 
-struct AnalyzeLds {
-  uint32_t data[kDataWords];       // the kG blocks, contiguous, + 16 B pad
-  uint64_t mask[kG][5];            // has_match bit per position
-  uint32_t head[kH];               // bucket -> last inserted position
-  uint32_t keys[kBlk + 4];         // 4-byte key per position (current block)
-  uint16_t nxt[kG][kBlk];          // circular bucket lists
+static_assert((kTB - 1) * kBlk + kInOff >= kTB * kBlkOutMax, "output overlay bound");
+static_assert(kInOff % 16 == 0 && kTileIn % 16 == 0, "16-B staging");
+
+// status word of a tile: epoch[63:40] | flag[39:38] | value[37:0]
+constexpr uint64_t kFlagAgg = 1, kFlagPre = 2;
+constexpr uint64_t kValMask = (1ull << 38) - 1;
+
+struct TileLds {
+  alignas(16) uint8_t buf[kRegion];
+  uint32_t head[kH];
+  uint32_t nxt[kArr];     // bucket cycles: entry of the next member
+  uint32_t rec[kArr];     // matchable p: M | dist<<8 | succ<<17
+  uint32_t seq[kArr];     // per sequence: cpos | end<<16; then pend | lit<<9
+  uint16_t nm[kArr];      // first matchable position >= x
+  uint16_t bsize[kTB];
 };
 
-__device__ __forceinline__ uint32_t load4u(const uint32_t *d, int off) {
+__device__ __forceinline__ uint32_t load4u(const uint8_t *b, int off) {
+  const uint32_t *d = reinterpret_cast<const uint32_t *>(b);
   const uint32_t w0 = d[off >> 2], w1 = d[(off >> 2) + 1];
   return __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(off & 3));
 }
 
-__device__ __forceinline__ uint32_t hash_key(uint32_t k) {
-  return (k * 2654435761u) >> kHashShift;
-}
-
 // Longest common prefix of the byte runs at a and b (a < b), capped at
-// `limit` = n - q: the canonical clamp (match never crosses the block end).
-__device__ __forceinline__ int lcp(const uint32_t *d, int a, int b, int limit) {
+// `limit` = n - b: the canonical clamp (a match never crosses the block end).
+// 8 bytes per step.
+__device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
   int l = 0;
   while (l < limit) {
-    const uint32_t x = load4u(d, a + l) ^ load4u(d, b + l);
-    if (x) {
-      l += __builtin_ctz(x) >> 3;
+    const uint32_t x0 = load4u(d, a + l) ^ load4u(d, b + l);
+    const uint32_t x1 = load4u(d, a + l + 4) ^ load4u(d, b + l + 4);
+    if (x0 | x1) {
+      l += x0 ? (__builtin_ctz(x0) >> 3) : 4 + (__builtin_ctz(x1) >> 3);
       return l < limit ? l : limit;
     }
-    l += 4;
+    l += 8;
   }
   return limit;
 }
@@ -93,275 +141,448 @@ __device__ __forceinline__ int seq_size_field(int L, int M) {
   return L + 5 + litext_len(L) + mext;
 }
 
-__global__ __launch_bounds__(64) void lz4_analyze(
-    const uint8_t *__restrict__ in, size_t n_total, size_t nb_total,
-    uint32_t *__restrict__ recs, uint32_t *__restrict__ info) {
-  __shared__ AnalyzeLds S;
-  const int lane = threadIdx.x;
-  const size_t b0 = (size_t)blockIdx.x * kG;
-  const int nb = (int)min((size_t)kG, nb_total - b0);
-  const size_t byte0 = b0 * kBlk;
-  const int len = (int)min((size_t)kChunkBytes, n_total - byte0);
-  const uint8_t *src = in + byte0;
-
-  // ---- stage the chunk in LDS (coalesced 16-B loads) ----------------------
-  uint8_t *lds_bytes = reinterpret_cast<uint8_t *>(S.data);
-  const int nvec = (((uintptr_t)src & 15) == 0) ? (len >> 4) : 0;
-  for (int i = lane; i < nvec; i += 64)
-    reinterpret_cast<uint4 *>(S.data)[i] = reinterpret_cast<const uint4 *>(src)[i];
-  for (int i = nvec * 16 + lane; i < len; i += 64) lds_bytes[i] = src[i];
-  if (lane < 16) lds_bytes[len + lane] = 0;
-  for (int i = lane; i < kH; i += 64) S.head[i] = kEmpty;
-  __syncthreads();
-
-  // ---- index phase: wave-parallel per block --------------------------------
-  for (int blk = 0; blk < nb; ++blk) {
-    const size_t gb = b0 + blk;
-    const int n = (gb == nb_total - 1) ? (int)(n_total - gb * kBlk) : kBlk;
-    const int nk = n >= 4 ? n - 3 : 0;      // positions that can start a >=4 match
-    const int base = blk * kBlk;
-    uint32_t key[5], hh[5];
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int p = r * 64 + lane;
-      key[r] = 0;
-      hh[r] = 0;
-      if (p < nk) {
-        key[r] = load4u(S.data, base + p);
-        hh[r] = hash_key(key[r]);
-        S.keys[p] = key[r];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int p = r * 64 + lane;
-      if (p < nk) S.nxt[blk][p] = (uint16_t)atomicExch(&S.head[hh[r]], (uint32_t)p);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {            // close each list into a cycle
-      const int p = r * 64 + lane;
-      if (p < nk && S.nxt[blk][p] == 0xFFFF) S.nxt[blk][p] = (uint16_t)S.head[hh[r]];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int p = r * 64 + lane;
-      bool found = false;
-      if (p < nk) {
-        int j = S.nxt[blk][p];
-        while (j != p) {
-          if (j < p && S.keys[j] == key[r]) { found = true; break; }
-          j = S.nxt[blk][j];
-        }
-      }
-      const uint64_t m = __ballot(found);
-      if (lane == 0) S.mask[blk][r] = m;
-    }
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int p = r * 64 + lane;
-      if (p < nk) S.head[hh[r]] = kEmpty;
-    }
-    __syncthreads();
-  }
-
-  // ---- parse phase: one lane per block -------------------------------------
-  if (lane < nb) {
-    const int blk = lane;
-    const size_t gb = b0 + blk;
-    const int n = (gb == nb_total - 1) ? (int)(n_total - gb * kBlk) : kBlk;
-    const int base = blk * kBlk;
-    uint32_t *out = recs + gb * kMaxRec;
-    int p = 0, L = 0, nrec = 0, W = 3;
-    while (true) {
-      int q = n;
-      for (int wi = p >> 6; wi < 5; ++wi) {           // next has_match >= p
-        uint64_t m = S.mask[blk][wi];
-        if (wi == (p >> 6)) m &= ~0ull << (p & 63);
-        if (m) { q = wi * 64 + __builtin_ctzll(m); break; }
-      }
-      if (q >= n) { L += n - p; break; }
-      L += q - p;
-      const int limit = n - q;
-      int best = 0, bj = 0;
-      int j = S.nxt[blk][q];
-      while (j != q) {                                // every equal-key i < q
-        if (j < q) {
-          const int l = lcp(S.data, base + j, base + q, limit);
-          if (l > best || (l == best && j < bj)) { best = l; bj = j; }
-        }
-        j = S.nxt[blk][j];
-      }
-      const int M = best >= 4 ? (best & 255) : 0;     // uint8_t return, LZ4.c:317
-      if (M == 0) {                                   // literal (len 256 -> 0)
-        L += 1;
-        p = q + 1;
-        if (p >= n) break;
-        continue;
-      }
-      out[nrec++] = (uint32_t)L | ((uint32_t)M << 9) | ((uint32_t)(q - bj) << 17);
-      W += seq_written(L, M);
-      L = 0;
-      p = q + M;                                      // LZ4.c:581
-      if (p >= n) break;
-    }
-    if (L > 0) {                                      // LZ4.c:585-613
-      out[nrec++] = (uint32_t)L;
-      W += seq_written(L, 0);
-    }
-    info[gb] = (uint32_t)W | ((uint32_t)nrec << 16);
-  }
+// DPP helpers (gfx9 row_shr / row_bcast; identity 0 for lanes without a source)
+template <int CTRL, int ROW, int BANK>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW, BANK, false);
 }
 
-// ---- exclusive scan of per-block byte counts (info & 0xFFFF) --------------
-constexpr int kScanThreads = 256;
-constexpr int kScanPer = 16;
-constexpr int kScanTile = kScanThreads * kScanPer;   // 4096 blocks per tile
-
-__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t o = __shfl_up(v, d, 64);
-    if (lane >= d) v += o;
-  }
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
+  v += dpp<0x111, 0xf, 0xf>(v);
+  v += dpp<0x112, 0xf, 0xf>(v);
+  v += dpp<0x114, 0xf, 0xf>(v);
+  v += dpp<0x118, 0xf, 0xf>(v);
+  v += dpp<0x142, 0xa, 0xf>(v);
+  v += dpp<0x143, 0xc, 0xf>(v);
   return v;
 }
 
-__global__ __launch_bounds__(kScanThreads) void lz4_scan_reduce(
-    const uint32_t *__restrict__ info, size_t nb, uint64_t *__restrict__ part) {
-  __shared__ uint64_t ws[kScanThreads / 64];
-  const size_t t0 = (size_t)blockIdx.x * kScanTile;
-  uint64_t s = 0;
-  for (int k = 0; k < kScanPer; ++k) {
-    const size_t i = t0 + (size_t)k * kScanThreads + threadIdx.x;
-    if (i < nb) s += info[i] & 0xFFFFu;
-  }
-  s = wave_incl_scan(s);
-  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  v = max(v, dpp<0x111, 0xf, 0xf>(v));
+  v = max(v, dpp<0x112, 0xf, 0xf>(v));
+  v = max(v, dpp<0x114, 0xf, 0xf>(v));
+  v = max(v, dpp<0x118, 0xf, 0xf>(v));
+  v = max(v, dpp<0x142, 0xa, 0xf>(v));
+  v = max(v, dpp<0x143, 0xc, 0xf>(v));
+  return v;
 }
 
-// single workgroup: exclusive scan of the tile partials; total -> *len
-__global__ __launch_bounds__(1024) void lz4_scan_partials(
-    uint64_t *__restrict__ part, size_t nparts, uint64_t hdr,
-    uint64_t *__restrict__ len) {
-  __shared__ uint64_t ws[16];
-  __shared__ uint64_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (size_t c0 = 0; c0 < nparts; c0 += 1024) {
-    const size_t i = c0 + threadIdx.x;
-    const uint64_t v = i < nparts ? part[i] : 0;
-    uint64_t s = wave_incl_scan(v);
-    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = s;
-    __syncthreads();
-    uint64_t pre = carry;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) pre += ws[w];
-    if (i < nparts) part[i] = pre + s - v;
-    __syncthreads();
-    if (threadIdx.x == 1023) carry = pre + s;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *len = hdr + carry;
+__device__ __forceinline__ uint32_t lane63(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-__global__ __launch_bounds__(kScanThreads) void lz4_scan_apply(
-    const uint32_t *__restrict__ info, size_t nb, const uint64_t *__restrict__ part,
-    uint64_t *__restrict__ off) {
-  __shared__ uint64_t ws[kScanThreads / 64];
-  const size_t t0 = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanPer;
-  uint32_t v[kScanPer];
-  uint64_t s = 0;
-  for (int k = 0; k < kScanPer; ++k) {
-    const size_t i = t0 + k;
-    v[k] = i < nb ? (info[i] & 0xFFFFu) : 0u;
-    s += v[k];
-  }
-  const uint64_t incl = wave_incl_scan(s);
-  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = incl;
-  __syncthreads();
-  uint64_t pre = part[blockIdx.x] + incl - s;
-  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) pre += ws[w];
-  for (int k = 0; k < kScanPer; ++k) {
-    const size_t i = t0 + k;
-    if (i < nb) off[i] = pre;
-    pre += v[k];
-  }
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
 }
 
-// ---- emit: one wave per block ----------------------------------------------
-__device__ __forceinline__ void put(uint8_t *out, uint64_t cap, uint64_t pos, uint8_t b) {
-  if (pos < cap) out[pos] = b;
-}
+__device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
 
-__global__ __launch_bounds__(256) void lz4_emit(
-    const uint8_t *__restrict__ in, size_t n_total, size_t nb_total,
-    const uint32_t *__restrict__ recs, const uint32_t *__restrict__ info,
-    const uint64_t *__restrict__ off, uint8_t *__restrict__ out, uint64_t cap,
-    int hdr) {
+__device__ __forceinline__ uint64_t lanemask_lt() {
   const int lane = threadIdx.x & 63;
-  const size_t b = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= nb_total) return;
-  if (hdr && b == 0 && lane == 0) put(out, cap, 0, (uint8_t)nb_total);  // LZ4.c:429
-  const int nrec = (int)(info[b] >> 16);
-  const uint64_t obase = (uint64_t)hdr + off[b];
-  const uint8_t *blk = in + b * kBlk;
-  const uint32_t *r = recs + b * kMaxRec;
+  return (1ull << lane) - 1ull;
+}
 
-  // packed (in_len:10 | written:11 | size_field:11) per record, two halves
-  int Lk[2], Mk[2], Dk[2];
-  uint32_t pk[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int k = h * 64 + lane;
-    const uint32_t rv = k < nrec ? r[k] : 0u;
-    Lk[h] = (int)(rv & 511u);
-    Mk[h] = (int)((rv >> 9) & 255u);
-    Dk[h] = (int)(rv >> 17);
-    pk[h] = 0;
-    if (k < nrec)
-      pk[h] = (uint32_t)(Lk[h] + Mk[h]) | ((uint32_t)seq_written(Lk[h], Mk[h]) << 10) |
-              ((uint32_t)seq_size_field(Lk[h], Mk[h]) << 21);
+// 16 bytes starting at byte `sb` (0..15, wave-uniform) of the 32-byte run lo:hi
+__device__ __forceinline__ uint4 funnel16(uint4 lo, uint4 hi, int sb) {
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const uint32_t by = (uint32_t)(sb & 3);
+  uint32_t x[5];
+  switch (sb >> 2) {
+    case 0: x[0] = w[0]; x[1] = w[1]; x[2] = w[2]; x[3] = w[3]; x[4] = w[4]; break;
+    case 1: x[0] = w[1]; x[1] = w[2]; x[2] = w[3]; x[3] = w[4]; x[4] = w[5]; break;
+    case 2: x[0] = w[2]; x[1] = w[3]; x[2] = w[4]; x[3] = w[5]; x[4] = w[6]; break;
+    default: x[0] = w[3]; x[1] = w[4]; x[2] = w[5]; x[3] = w[6]; x[4] = w[7]; break;
   }
-  uint32_t inc0 = (uint32_t)wave_incl_scan(pk[0]);
-  const uint32_t tot0 = __shfl(inc0, 63, 64);
-  uint32_t inc1 = (uint32_t)wave_incl_scan(pk[1]) + tot0;
-  const uint32_t tot = __shfl(inc1, 63, 64);
-  if (lane == 0) {                                                  // LZ4.c:417-419
-    const uint32_t bsize = (tot >> 21) + 3;
-    put(out, cap, obase + 0, (uint8_t)nrec);
-    put(out, cap, obase + 1, (uint8_t)(bsize & 255));
-    put(out, cap, obase + 2, (uint8_t)((bsize >> 8) & 255));
-  }
+  return make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], by),
+                    __builtin_amdgcn_alignbyte(x[2], x[1], by),
+                    __builtin_amdgcn_alignbyte(x[3], x[2], by),
+                    __builtin_amdgcn_alignbyte(x[4], x[3], by));
+}
+
+__device__ __forceinline__ uint64_t status_load(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void status_store(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Encode block `k` of the tile (n bytes at S.buf[kInOff + 300k]) into
+// S.buf[obase ...]; returns the bytes written.
+__device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
+                                            uint64_t *prof, uint64_t &prof_last) {
+  (void)prof; (void)prof_last;
+  const int lane = threadIdx.x;
+  const int base = kInOff + k * kBlk;
+
+  // ---- index: chain every 4-gram start into its bucket --------------------
+  uint32_t key[5], ent[5], hb[5];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int k = h * 64 + lane;
-    if (k >= nrec) continue;
-    const uint32_t excl = (h ? inc1 : inc0) - pk[h];
-    const int L = Lk[h], M = Mk[h], D = Dk[h];
-    const int lit = (int)(excl & 1023u);
-    uint64_t o = obase + 3 + ((excl >> 10) & 2047u);
-    const int S = seq_size_field(L, M);
-    const int tl = L >= 15 ? 15 : L;                                // LZ4.c:540
-    const int tm = M == 0 ? 0 : (M >= 19 ? 15 : ((M - 4) & 255));   // LZ4.c:542
-    put(out, cap, o++, (uint8_t)((tl << 4) | tm));                  // LZ4.c:367
-    put(out, cap, o++, (uint8_t)(S & 255));                         // LZ4.c:369
-    put(out, cap, o++, (uint8_t)((S >> 8) & 255));
-    if (L >= 15) {                                                  // LZ4.c:372-386
-      const int rem = (L - 15) & 255;
-      if (rem == 255) { put(out, cap, o++, 255); put(out, cap, o++, 0); }
-      else put(out, cap, o++, (uint8_t)rem);
+  for (int r = 0; r < 5; ++r) {
+    const int p = r * 64 + lane;
+    key[r] = p < n ? load4u(S.buf, base + p) : 0u;
+    const uint32_t pb = p >= 1 && p < n ? (uint32_t)S.buf[base + p - 1] : 0u;
+    const uint32_t hm = key[r] * 2654435761u;
+    hb[r] = hm >> (32 - kHB);
+    ent[r] = (uint32_t)p | (pb << 9) | (((hm >> 8) & 0x7FFFu) << 17);
+  }
+  uint32_t old[5];
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int p = r * 64 + lane;
+    old[r] = kEmpty;
+    if (p < n) S.rec[p] = 0u;            // local(p) accumulator
+    if ((LZ4R_VARIANT < 2 || LZ4R_VARIANT == 4) && p + 4 <= n) {
+      old[r] = atomicExch(&S.head[hb[r]], ent[r]);
+      S.nxt[p] = old[r];
     }
-    for (int i = 0; i < L; ++i) put(out, cap, o++, blk[lit + i]);  // LZ4.c:388
-    put(out, cap, o++, (uint8_t)(D & 255));                         // LZ4.c:390
-    put(out, cap, o++, (uint8_t)((D >> 8) & 255));
-    if (M >= 4 && ((M - 4) & 255) >= 15)                            // LZ4.c:393-411
-      put(out, cap, o++, (uint8_t)(((M - 4) & 255) - 15));
   }
+  __syncthreads();
+  uint32_t todo = 0;                     // rounds whose bucket has other members
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {          // close each bucket list into a cycle
+    const int p = r * 64 + lane;
+    if (p + 4 <= n) {
+      bool alone = false;
+      if ((old[r] & 511u) == 511u) {
+        const uint32_t h = S.head[hb[r]];
+        S.nxt[p] = h;
+        alone = h == ent[r];
+      }
+      if (!alone) todo |= 1u << r;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {          // head is not read again in this block
+    const int p = r * 64 + lane;
+    if (p + 4 <= n) S.head[hb[r]] = kEmpty;
+  }
+  if (LZ4R_VARIANT != 0 && LZ4R_VARIANT != 4) todo = 0;
+
+  PROF_T(0);
+  // ---- local(p): left-maximal candidates -> list -> lcp -> atomicMax -------
+  // One cursor per lane walks the lane's non-singleton bucket cycles one
+  // after another (one LDS read per step); candidate pairs (p, j) go to a
+  // wave list in S.seq, drained by a balanced lcp pass.
+  {
+    int r = todo ? __builtin_ctz(todo) : 5;
+    uint32_t me = 0, cur = 0;
+    auto pick = [&](int rr) {
+      return rr == 0 ? ent[0] : rr == 1 ? ent[1] : rr == 2 ? ent[2] : rr == 3 ? ent[3] : ent[4];
+    };
+    if (r < 5) {
+      me = pick(r);
+      cur = S.nxt[r * 64 + lane];
+    }
+    int cnt = 0;
+    auto drain = [&]() {
+      __syncthreads();
+      for (int i = lane; i < cnt; i += 64) {
+        const uint32_t pr = S.seq[i];
+        const int p = (int)(pr & 0xFFFFu), j = (int)(pr >> 16);
+        const int l = lcp(S.buf, base + j, base + p, n - p);
+        if (l >= 4) atomicMax(&S.rec[p], ((uint32_t)l << 9) | (uint32_t)(511 - j));
+      }
+      __syncthreads();
+    };
+    // Branch-free body: every lane issues exactly one LDS read per step from
+    // an always-valid address; non-candidates write to the trash slot.
+    constexpr int kTrash = kArr - 1;
+    while (__ballot(r < 5)) {
+      const bool act = r < 5;
+      const int p = r * 64 + lane;
+      const int jp = (int)(cur & 511u);
+      const bool done = act && jp == p;
+      const uint32_t x = cur ^ me;
+      const bool cand = act && jp < p && (x >> 17) == 0 &&
+                        (jp == 0 || (x & (255u << 9)) != 0);
+      const uint64_t cm = __ballot(cand);
+      const int slot = cand ? cnt + __popcll(cm & lanemask_lt()) : kTrash;
+      S.seq[slot] = (uint32_t)p | ((uint32_t)jp << 16);
+      cnt += __popcll(cm);
+      const uint32_t todo2 = done ? (todo & ~(1u << r)) : todo;
+      const int rn = todo2 ? __builtin_ctz(todo2) : 5;
+      const int r2 = done ? rn : r;
+      todo = todo2;
+      me = done ? pick(r2) : me;
+      const int addr = done ? (r2 < 5 ? r2 * 64 + lane : lane) : (act ? jp : lane);
+      cur = S.nxt[addr];
+      r = r2;
+      if (cnt > kTrash - 64) {
+        drain();
+        cnt = 0;
+      }
+    }
+    PROF_T(1);
+    if (cnt) drain();
+    PROF_T(2);
+  }
+  __syncthreads();
+  int bl[5], bj[5];
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int p = r * 64 + lane;
+    const uint32_t v = p < n ? S.rec[p] : 0u;
+    bl[r] = (int)(v >> 9);
+    bj[r] = 511 - (int)(v & 511u);
+  }
+
+  // ---- best(p) = prefix lexmax of (end, dist) -------------------------------
+  uint32_t mrec[5];
+  uint64_t mask[5];
+  uint32_t carry = 0;
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int p = r * 64 + lane;
+    uint32_t v = bl[r] >= 4 ? (((uint32_t)(p + bl[r]) << 9) | (uint32_t)(p - bj[r])) : 0u;
+    v = max(wave_incl_max(v), carry);
+    carry = lane63(v);
+    const int len = (int)(v >> 9) - p;                  // >= 4 iff a match starts here
+    const int M = len >= 4 ? (len & 255) : 0;           // uint8_t return, LZ4.c:317
+    mrec[r] = (uint32_t)M | ((v & 511u) << 8);
+    mask[r] = __ballot(M != 0);
+  }
+
+  // ---- nm(x): first matchable position >= x, for x in [0, n] ---------------
+  int F[6];
+  F[5] = n;
+#pragma unroll
+  for (int r = 4; r >= 0; --r) F[r] = mask[r] ? r * 64 + ctz64(mask[r]) : F[r + 1];
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int p = r * 64 + lane;
+    if (p <= n) {
+      const uint64_t m = mask[r] & (~0ull << lane);
+      S.nm[p] = (uint16_t)(m ? r * 64 + ctz64(m) : F[r + 1]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int p = r * 64 + lane;
+    const int M = (int)(mrec[r] & 255u);
+    if (M != 0) S.rec[p] = mrec[r] | ((uint32_t)S.nm[p + M] << 17);
+  }
+  __syncthreads();
+
+  PROF_T(3);
+  // ---- greedy parse = walk over match starts (LZ4.c:516-583) ---------------
+  uint64_t V0 = 0, V1 = 0, V2 = 0, V3 = 0, V4 = 0;      // visited match starts
+  int c = F[0], e = 0, Sv = 0;
+  while (c < n) {
+    const uint32_t rv = __builtin_amdgcn_readfirstlane(S.rec[c]);
+    e = c + (int)(rv & 255u);
+    if (lane == 0) S.seq[Sv] = (uint32_t)c | ((uint32_t)e << 16);
+    const uint64_t bit = 1ull << (c & 63);
+    switch (c >> 6) {
+      case 0: V0 |= bit; break;
+      case 1: V1 |= bit; break;
+      case 2: V2 |= bit; break;
+      case 3: V3 |= bit; break;
+      default: V4 |= bit; break;
+    }
+    ++Sv;
+    c = (int)(rv >> 17);
+  }
+  const uint64_t V[5] = {V0, V1, V2, V3, V4};
+  __syncthreads();
+
+  PROF_T(4);
+  // ---- sequences: lane kk = sequence kk ------------------------------------
+  const int nseq = Sv + (e < n ? 1 : 0);
+  int ocar = 3;                      // block header: u8 nseq, u16 size
+  int szsum = 0;
+  int end_prev = 0;                  // end of the previous round's last match
+  for (int s0 = 0; s0 < nseq; s0 += 64) {
+    const int kk = s0 + lane;
+    const bool act = kk < nseq;
+    int M = 0, D = 0, cpos = n, end = n;
+    if (act && kk < Sv) {
+      const uint32_t sq = S.seq[kk];
+      cpos = (int)(sq & 0xFFFFu);
+      end = (int)(sq >> 16);
+      const uint32_t rv = S.rec[cpos];
+      M = (int)(rv & 255u);
+      D = (int)((rv >> 8) & 511u);
+    }
+    const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
+    const int pend = lane == 0 ? end_prev : (int)upv;             // literal run start
+    end_prev = (int)lane63((uint32_t)end);
+    const int L = cpos - pend;
+    const int W = act ? seq_written(L, M) : 0;
+    const int SZ = act ? seq_size_field(L, M) : 0;
+    const uint32_t inc = wave_incl_add((uint32_t)W | ((uint32_t)SZ << 16));
+    const uint32_t tot = lane63(inc);
+    const int excl = (int)(inc & 0xFFFFu) - W;
+    if (act) {
+      int o = obase + ocar + excl;
+      const int tl = L >= 15 ? 15 : L;                                // LZ4.c:540
+      const int tm = M == 0 ? 0 : (M >= 19 ? 15 : ((M - 4) & 255));   // LZ4.c:542
+      S.buf[o++] = (uint8_t)((tl << 4) | tm);                          // LZ4.c:367
+      S.buf[o++] = (uint8_t)(SZ & 255);                                // LZ4.c:369
+      S.buf[o++] = (uint8_t)((SZ >> 8) & 255);
+      if (L >= 15) {                                                   // LZ4.c:372-386
+        const int rem = (L - 15) & 255;
+        if (rem == 255) { S.buf[o++] = 255; S.buf[o++] = 0; }
+        else S.buf[o++] = (uint8_t)rem;
+      }
+      S.seq[kk] = (uint32_t)pend | ((uint32_t)(o - pend + 512) << 9);  // literal dest
+      o += L;                                                          // LZ4.c:388
+      S.buf[o++] = (uint8_t)(D & 255);                                 // LZ4.c:390
+      S.buf[o++] = (uint8_t)((D >> 8) & 255);
+      if (M >= 4 && ((M - 4) & 255) >= 15)                             // LZ4.c:393-411
+        S.buf[o++] = (uint8_t)(((M - 4) & 255) - 15);
+    }
+    ocar += (int)(tot & 0xFFFFu);
+    szsum += (int)(tot >> 16);
+  }
+  if (lane == 0) {                                                     // LZ4.c:417-419
+    const int bsz = szsum + 3;
+    S.buf[obase] = (uint8_t)nseq;
+    S.buf[obase + 1] = (uint8_t)(bsz & 255);
+    S.buf[obase + 2] = (uint8_t)((bsz >> 8) & 255);
+    // positions inside a block-final match rank to sequence Sv: when there
+    // is no literal tail, that slot gets pend = n so they are never scattered
+    if (e >= n) S.seq[Sv] = (uint32_t)n;
+  }
+  __syncthreads();
+
+  PROF_T(5);
+  // ---- literal bytes: position-parallel scatter ----------------------------
+  int preV = 0;
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int p = r * 64 + lane;
+    if (p < n && !((V[r] >> lane) & 1ull)) {
+      const int kk = preV + __popcll(V[r] & lanemask_lt());
+      const uint32_t sl = S.seq[kk];
+      const int pend = (int)(sl & 511u);
+      if (p >= pend) S.buf[(int)(sl >> 9) - 512 + p] = (uint8_t)(key[r] & 255u);
+    }
+    preV += __popcll(V[r]);
+  }
+  __syncthreads();
+  PROF_T(6);
+  return ocar;
+}
+
+__global__ __launch_bounds__(64) void lz4_tiles(
+    const uint8_t *__restrict__ in, size_t n_total, size_t nb_total, size_t ntiles,
+    uint8_t *__restrict__ out, uint64_t cap, int hdr, uint64_t *__restrict__ d_len,
+    uint16_t *__restrict__ bsizes, uint64_t *__restrict__ status, uint64_t epoch) {
+  __shared__ TileLds S;
+  const int lane = threadIdx.x;
+  uint64_t prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef LZ4R_PROF
+  uint64_t prof_last = prof_now();
+#else
+  uint64_t prof_last = 0;
+#endif
+
+  for (int i = lane; i < kH; i += 64) S.head[i] = kEmpty;
+
+  for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const size_t b0 = t * kTB;
+    const int nbt = (int)min((size_t)kTB, nb_total - b0);
+    const size_t byte0 = b0 * kBlk;
+    const int len = (int)min((size_t)kTileIn, n_total - byte0);
+    const uint8_t *src = in + byte0;
+
+    // ---- stage the tile (16-B loads) ---------------------------------------
+    {
+      uint8_t *dst = S.buf + kInOff;
+      const int nvec = (((uintptr_t)src & 15) == 0) ? (len >> 4) : 0;
+      for (int i = lane; i < nvec; i += 64)
+        reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+      for (int i = nvec * 16 + lane; i < len; i += 64) dst[i] = src[i];
+      if (lane < 16) dst[len + lane] = 0;
+    }
+    __syncthreads();
+
+    // ---- encode the tile's blocks ------------------------------------------
+    int obase = 0;
+    for (int k = 0; k < nbt; ++k) {
+      const size_t gb = b0 + k;
+      const int n = (gb == nb_total - 1) ? (int)(n_total - gb * kBlk) : kBlk;
+      PROF_T(7);
+      const int W = encode_block(S, k, n, obase, prof, prof_last);
+      if (lane == 0) S.bsize[k] = (uint16_t)W;
+      obase += W;
+    }
+    __syncthreads();
+    if (lane < nbt) bsizes[b0 + lane] = S.bsize[lane];
+
+    PROF_T(7);
+    // ---- decoupled look-back: exclusive byte offset of this tile ------------
+    const uint64_t agg = (uint64_t)obase;
+    const uint64_t ep = epoch << 40;
+    uint64_t excl = 0;
+    if (LZ4R_VARIANT >= 3) {
+      excl = t * (uint64_t)kTB * kBlkOutMax;
+    } else if (t == 0) {
+      if (lane == 0) status_store(&status[0], ep | (kFlagPre << 38) | agg);
+    } else {
+      if (lane == 0) status_store(&status[t], ep | (kFlagAgg << 38) | agg);
+      long long j = (long long)t - 1;               // closest predecessor not yet summed
+      while (true) {
+        const long long idx = j - lane;
+        uint64_t s = ep | (kFlagPre << 38);         // before tile 0: prefix 0
+        if (idx >= 0) s = status_load(&status[idx]);
+        const bool ready = (s >> 40) == epoch && ((s >> 38) & 3u) != 0;
+        const bool pre = ready && ((s >> 38) & 3u) == kFlagPre;
+        const uint64_t pmask = __ballot(pre);
+        const uint64_t nready = __ballot(!ready);
+        const int fp = pmask ? ctz64(pmask) : 64;   // nearest inclusive prefix
+        const uint64_t need = fp >= 63 ? ~0ull : ((2ull << fp) - 1ull);
+        if (nready & need) {                        // a needed predecessor is not out yet
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        const uint64_t v = (lane <= fp) ? (s & kValMask) : 0;
+        excl += wave_sum64(v);
+        if (fp < 64) break;
+        j -= 64;
+      }
+      if (lane == 0) status_store(&status[t], ep | (kFlagPre << 38) | ((excl + agg) & kValMask));
+    }
+    if (t == ntiles - 1 && lane == 0) *d_len = (uint64_t)hdr + excl + agg;
+    if (hdr && t == 0 && lane == 0 && cap > 0) out[0] = (uint8_t)nb_total;   // LZ4.c:429
+
+    PROF_T(8);
+    // ---- store: LDS -> HBM as aligned 16-B chunks ----------------------------
+    const uint64_t o0 = (uint64_t)hdr + excl;
+    const uint64_t o1 = min(o0 + agg, cap);
+    if (o1 > o0) {
+      const uintptr_t abs0 = (uintptr_t)(out + o0);
+      const uintptr_t first = abs0 & ~(uintptr_t)15;
+      const uintptr_t absend = (uintptr_t)(out + o1);
+      const int shift = (int)(abs0 - first);        // uniform: 0..15
+      const int nchunks = (int)((absend - first + 15) >> 4);
+      for (int ci = lane; ci < nchunks; ci += 64) {
+        const uintptr_t a = first + ((uintptr_t)ci << 4);
+        const int s = ci * 16 - shift;              // LDS byte of chunk start
+        if (a >= abs0 && a + 16 <= absend) {
+          // bytes s .. s+15 lie in the 32 B at s & ~15; s & 15 is uniform
+          const uint4 *q = reinterpret_cast<const uint4 *>(S.buf + (s & ~15));
+          const uint4 lo = q[0], hi = q[1];
+          *reinterpret_cast<uint4 *>(a) = funnel16(lo, hi, s & 15);
+        } else {
+          for (int b = 0; b < 16; ++b) {
+            const uintptr_t ab = a + b;
+            if (ab >= abs0 && ab < absend) *reinterpret_cast<uint8_t *>(ab) = S.buf[s + b];
+          }
+        }
+      }
+    }
+    __syncthreads();                                // LDS reused by the next tile
+    PROF_T(9);
+  }
+#ifdef LZ4R_PROF
+  if (lane == 0)
+    for (int i = 0; i < 10; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof[i]);
+#endif
 }
 
 }  // namespace
@@ -369,11 +590,13 @@ __global__ __launch_bounds__(256) void lz4_emit(
 struct lz4r_ctx {
   int device = 0;
   size_t cap_blocks = 0;       // capacity of the per-block arrays
-  uint32_t *recs = nullptr;
-  uint32_t *info = nullptr;
-  uint64_t *off = nullptr;
-  uint64_t *part = nullptr;
+  size_t cap_tiles = 0;
+  uint16_t *bsizes = nullptr;  // encoded bytes of every block of the last call
+  uint64_t *status = nullptr;  // look-back words, one per tile
+  uint64_t epoch = 0;
+  unsigned max_grid = 0;       // co-resident workgroups of lz4_tiles on this device
   uint64_t *len = nullptr;     // default device length slot
+  size_t last_nb = 0;
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr;
   bool timing = false;
   bool timed_call = false;     // the last call recorded the events
@@ -382,27 +605,28 @@ struct lz4r_ctx {
 namespace {
 
 void free_scratch(lz4r_ctx *c) {
-  (void)hipFree(c->recs);
-  (void)hipFree(c->info);
-  (void)hipFree(c->off);
-  (void)hipFree(c->part);
-  c->recs = nullptr; c->info = nullptr; c->off = nullptr; c->part = nullptr;
+  (void)hipFree(c->bsizes);
+  (void)hipFree(c->status);
+  c->bsizes = nullptr;
+  c->status = nullptr;
   c->cap_blocks = 0;
+  c->cap_tiles = 0;
 }
 
 int ensure_scratch(lz4r_ctx *c, size_t nb) {
   if (nb <= c->cap_blocks) return LZ4R_OK;
   free_scratch(c);
   const size_t cap = nb + nb / 8 + 1024;
-  const size_t nparts = (cap + kScanTile - 1) / kScanTile;
-  if (hipMalloc(&c->recs, cap * kMaxRec * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&c->info, cap * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&c->off, cap * sizeof(uint64_t)) != hipSuccess ||
-      hipMalloc(&c->part, (nparts + 1) * sizeof(uint64_t)) != hipSuccess) {
+  const size_t tiles = (cap + kTB - 1) / kTB;
+  if (hipMalloc(&c->bsizes, cap * sizeof(uint16_t)) != hipSuccess ||
+      hipMalloc(&c->status, tiles * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->status, 0, tiles * sizeof(uint64_t)) != hipSuccess) {
     free_scratch(c);
     return LZ4R_ERR_NOMEM;
   }
+  c->epoch = 0;                // fresh (zeroed) status words: epochs restart
   c->cap_blocks = cap;
+  c->cap_tiles = tiles;
   return LZ4R_OK;
 }
 
@@ -414,26 +638,27 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   const size_t nb = (n + kBlk - 1) / kBlk;
   int rc = ensure_scratch(c, nb);
   if (rc != LZ4R_OK) return rc;
+  const size_t ntiles = (nb + kTB - 1) / kTB;
+  if (ntiles > 0xffffffffULL || n > (1ull << 37)) return LZ4R_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const size_t ntiles = (nb + kScanTile - 1) / kScanTile;
-  const size_t ga = (nb + kG - 1) / kG;
-  if (ga > 0x7fffffffULL) return LZ4R_ERR_ARG;
+  if (++c->epoch >= (1ull << 24)) {                 // epoch wrap: clear the words
+    if (hipMemsetAsync(c->status, 0, c->cap_tiles * sizeof(uint64_t), s) != hipSuccess)
+      return LZ4R_ERR_HIP;
+    c->epoch = 1;
+  }
   const bool timed = c->timing;
   c->timed_call = timed;
   if (timed) (void)hipEventRecord(c->ev_a, s);
-  hipLaunchKernelGGL(lz4_analyze, dim3((unsigned)ga), dim3(64), 0, s,
-                     static_cast<const uint8_t *>(d_in), n, nb, c->recs, c->info);
-  if (timed) (void)hipEventRecord(c->ev_b, s);
-  hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s,
-                     c->info, nb, c->part);
-  hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part, ntiles,
-                     (uint64_t)hdr, static_cast<uint64_t *>(d_len));
-  hipLaunchKernelGGL(lz4_scan_apply, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s,
-                     c->info, nb, c->part, c->off);
-  hipLaunchKernelGGL(lz4_emit, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s,
-                     static_cast<const uint8_t *>(d_in), n, nb, c->recs, c->info, c->off,
-                     static_cast<uint8_t *>(d_out), (uint64_t)cap, hdr);
-  if (timed) (void)hipEventRecord(c->ev_c, s);
+  const unsigned grid = (unsigned)(ntiles < c->max_grid ? ntiles : c->max_grid);
+  hipLaunchKernelGGL(lz4_tiles, dim3(grid), dim3(64), 0, s,
+                     static_cast<const uint8_t *>(d_in), n, nb, ntiles,
+                     static_cast<uint8_t *>(d_out), (uint64_t)cap, hdr,
+                     static_cast<uint64_t *>(d_len), c->bsizes, c->status, c->epoch);
+  if (timed) {
+    (void)hipEventRecord(c->ev_b, s);
+    (void)hipEventRecord(c->ev_c, s);
+  }
+  c->last_nb = nb;
   return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
 }
 
@@ -441,17 +666,33 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
 
 extern "C" {
 
+#ifdef LZ4R_PROF
+int lz4r_debug_prof(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int lz4r_ctx_create(lz4r_ctx **out) {
   if (!out) return LZ4R_ERR_ARG;
   lz4r_ctx *c = new (std::nothrow) lz4r_ctx();
   if (!c) return LZ4R_ERR_NOMEM;
+  int cus = 0, occ = 0;
   if (hipGetDevice(&c->device) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lz4_tiles, 64, 0) != hipSuccess ||
+      cus <= 0 || occ <= 0 ||
       hipMalloc(&c->len, sizeof(uint64_t)) != hipSuccess ||
       hipEventCreate(&c->ev_a) != hipSuccess || hipEventCreate(&c->ev_b) != hipSuccess ||
       hipEventCreate(&c->ev_c) != hipSuccess) {
     lz4r_ctx_destroy(c);
     return LZ4R_ERR_HIP;
   }
+  // The look-back needs every workgroup of the grid resident at once (a tile
+  // waits on lower tiles only; each workgroup walks its tiles in order).
+  // One workgroup per CU of margin under the occupancy answer.
+  const int per_cu = occ > 1 ? occ - 1 : 1;
+  c->max_grid = (unsigned)(per_cu * cus);
   *out = c;
   return LZ4R_OK;
 }
@@ -494,11 +735,28 @@ int lz4r_compress_device(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, s
   return need > cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
 }
 
-int lz4r_copy_block_offsets(const lz4r_ctx *c, void *dst, size_t count, void *stream) {
-  if (!c || !dst || count > c->cap_blocks) return LZ4R_ERR_ARG;
+int lz4r_copy_block_sizes(const lz4r_ctx *c, void *dst, size_t count, void *stream) {
+  if (!c || !dst || count > c->last_nb) return LZ4R_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipMemcpyAsync(dst, c->off, count * sizeof(uint64_t), hipMemcpyDefault, s) != hipSuccess ||
+  if (hipMemcpyAsync(dst, c->bsizes, count * sizeof(uint16_t), hipMemcpyDefault, s) !=
+          hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
+    return LZ4R_ERR_HIP;
+  return LZ4R_OK;
+}
+
+int lz4r_copy_block_offsets(const lz4r_ctx *c, void *dst, size_t count, void *stream) {
+  if (!c || !dst || count > c->last_nb) return LZ4R_ERR_ARG;
+  std::vector<uint16_t> sz(count);
+  std::vector<uint64_t> off(count);
+  int rc = lz4r_copy_block_sizes(c, sz.data(), count, stream);
+  if (rc != LZ4R_OK) return rc;
+  uint64_t acc = 0;
+  for (size_t i = 0; i < count; ++i) {
+    off[i] = acc;
+    acc += sz[i];
+  }
+  if (hipMemcpy(dst, off.data(), count * sizeof(uint64_t), hipMemcpyDefault) != hipSuccess)
     return LZ4R_ERR_HIP;
   return LZ4R_OK;
 }

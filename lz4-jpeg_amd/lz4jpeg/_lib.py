@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblz4jpeg.so")
+LIB_PATH = os.environ.get("LZ4JPEG_LIB") or os.path.join(_HERE, "liblz4jpeg.so")
 
 _c_size = ctypes.c_size_t
 _vp = ctypes.c_void_p
@@ -24,6 +24,7 @@ SIGNATURES = [
     ("lz4r_compress_device", _i, [_vp, _vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size), _vp]),
     ("lz4r_compress_async", _i, [_vp, _vp, _c_size, _vp, _c_size, _vp, _vp]),
     ("lz4r_compress_segment_async", _i, [_vp, _vp, _c_size, _vp, _c_size, _vp, _vp]),
+    ("lz4r_copy_block_sizes", _i, [_vp, _vp, _c_size, _vp]),
     ("lz4r_copy_block_offsets", _i, [_vp, _vp, _c_size, _vp]),
     ("lz4r_compress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
     ("lz4r_set_timing", _i, [_vp, _i]),
