@@ -2,42 +2,62 @@
 # cross-compiles; the built .so / executables travel to the GPU box in-tree.
 #
 #   lz4-jpeg_amd/lz4jpeg/liblz4jpeg.so   product C-ABI library (HIP kernels)
-#   lz4-jpeg_amd/bin/LZ4_seq, JPEG_seq    drop-in executables (file contract)
+#   lz4-jpeg_amd/bin/LZ4_seq, JPEG_seq    drop-in executables (file contract),
+#                                         also as LZ4_seq.exe / JPEG_seq.exe
 #   oracle/liboracle.so (+ oracle/_ref)   test-only CPU checker
 HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
 CC      ?= gcc
 PKG     := lz4-jpeg_amd
 CSRC    := $(PKG)/csrc
+HOST    := $(PKG)/host
+B       := $(PKG)/build
+BIN     := $(PKG)/bin
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -ffp-contract=off -fPIC -std=c++17 -Wall \
             -Wno-unused-result
+CFLAGS_HOST := -O2 -fPIC -Wall -std=gnu11 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
 LIB     := $(PKG)/lz4jpeg/liblz4jpeg.so
-HIP_SRC := $(CSRC)/lz4r.hip $(CSRC)/jpegr.hip
-HDRS    := include/lz4r.h include/jpegr.h $(CSRC)/jpeg_tables.h
+HDRS    := include/lz4r.h include/jpegr.h include/lz4jpeg_compat.h $(CSRC)/jpeg_tables.h
+OBJS    := $(B)/lz4r.o $(B)/jpegr.o $(B)/jpegr_blocks.o $(B)/synth.o $(B)/lz4r_decode.o \
+           $(B)/compat.o
 
-all: lib oracle
+all: lib bin oracle
 
 lib: $(LIB)
+
+bin: $(BIN)/LZ4_seq $(BIN)/JPEG_seq $(BIN)/LZ4_seq.exe $(BIN)/JPEG_seq.exe
 
 $(CSRC)/jpeg_tables.h: $(CSRC)/gen_jpeg_tables.py
 	python3 $< > $@
 
-$(PKG)/build/%.o: $(CSRC)/%.hip $(HDRS)
-	@mkdir -p $(PKG)/build
+$(B)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(B)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(PKG)/build/synth.o: $(PKG)/host/synth.c
-	@mkdir -p $(PKG)/build
-	$(CC) -O2 -fPIC -Wall -c $< -o $@
+$(B)/%.o: $(HOST)/%.c $(HDRS) $(HOST)/lzj_host.h
+	@mkdir -p $(B)
+	$(CC) $(CFLAGS_HOST) -c $< -o $@
 
-$(LIB): $(PKG)/build/lz4r.o $(PKG)/build/jpegr.o $(PKG)/build/synth.o
+$(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+# executables link the objects statically (no liblz4jpeg.so lookup at run time)
+$(BIN)/LZ4_seq: $(B)/lz4_seq.o $(OBJS)
+	@mkdir -p $(BIN)
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^
+
+$(BIN)/JPEG_seq: $(B)/jpeg_seq.o $(B)/png_io.o $(OBJS)
+	@mkdir -p $(BIN)
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -lz
+
+$(BIN)/%.exe: $(BIN)/%
+	cp $< $@
 
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(PKG)/build $(LIB)
+	rm -rf $(B) $(BIN) $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle clean
+.PHONY: all lib bin oracle clean

@@ -28,6 +28,19 @@ for _p in (os.path.join(REPO, "lz4-jpeg_amd"), os.path.join(REPO, "tests")):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+# (tools/traffic.sh -> tools/traffic_summary.py, gfx950 FETCH correction applied)
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r01_traffic.json")
+
+
+def measured_traffic(kind, bytes_now, bytes_profiled):
+    """HBM bytes per launch of the profiled kernel, scaled to this launch's
+    input size (the profile ran the same configuration), or None."""
+    try:
+        t = json.load(open(TRAFFIC_JSON))[kind]
+    except (OSError, KeyError, ValueError):
+        return None
+    return int(round(t["traffic_bytes"] * bytes_now / bytes_profiled))
 FP64_VALU_PEAK_TOPS = 39.3     # 78.6 TFLOPS fp64 vector spec counts FMA as 2
 
 
@@ -138,15 +151,18 @@ def main():
         gather_ms = max_over_ranks(time.perf_counter() - g0) * 1e3
 
     roof_lz4 = {
-        "bound": "hbm", "kernel": "lz4_analyze",
+        "bound": "hbm", "kernel": "lz4_tiles",
         "achieved": round(n / (avg_match_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
         "unit": "GB/s", "frac": round(n / (avg_match_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-        "traffic": None,
+        "traffic": measured_traffic("lz4", n, 1 << 30),
         "algorithmic_bytes_per_launch": n,
         "avg_launch_ms": round(avg_match_ms, 4),
         "whole_call_ms": round(avg_call_ms, 4),
-        "note": "algorithmic bytes = 1 B read per input byte (SURVEY §8d); HIP events on the "
-                "launch stream around lz4_analyze inside each timed step",
+        "note": "algorithmic bytes = 1 B read per input byte (SURVEY §8d: the HBM-read "
+                "roofline); achieved = that / lz4_tiles time from HIP events on its launch "
+                "stream in each timed step; traffic = FETCH_SIZE(x2, gfx950) + WRITE_SIZE "
+                "per launch from profiles/r01_traffic.json; the kernel is issue-bound "
+                "(DESIGN.md), not HBM-bound",
     }
 
     # ----------------------------------------------------------------- JPEG
@@ -187,7 +203,8 @@ def main():
                 "bound": "hbm", "kernel": "jpeg_strip_kernel",
                 "achieved": round(8 * px_rank / (kern_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(8 * px_rank / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                "traffic": None, "algorithmic_bytes_per_launch": 8 * px_rank,
+                "traffic": measured_traffic("jpeg", px_rank, 3840 * 2160),
+                "algorithmic_bytes_per_launch": 8 * px_rank,
                 "avg_launch_ms": round(kern_ms, 4),
                 "binding_roof": {
                     "bound": "valu_fp64", "unit": "Tops/s",
@@ -197,7 +214,8 @@ def main():
                     "note": "13312 non-fused fp64 mul/add per tile in reference order "
                             "(8704 luma + 2x2304 chroma); peak = 78.6 TF fp64 vector spec / 2",
                 },
-                "note": "8 B/pixel algorithmic (4 B RGBA read + 4 B int16 written)",
+                "note": "8 B/pixel algorithmic (4 B RGBA read + 4 B int16 written); traffic "
+                        "from profiles/r01_traffic.json (PMC FETCH_SIZE x2 + WRITE_SIZE)",
             },
         }
         log(f"jpeg: {jres['ms_per_step']} ms/step, {gpix:.2f} Gpix/s aggregate, kernel {kern_ms:.4f} ms")

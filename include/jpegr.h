@@ -66,6 +66,27 @@ int jpegr_time_device(const void *d_rgba, int w, int h, int nimg,
                       void *d_out_i16, int iters, void *stream,
                       float *ms_per_launch);
 
+/* Block-level kernels (jpegr_blocks.hip) behind the reference-named API in
+ * lz4jpeg_compat.h, asynchronous on `stream`:
+ *   jpegr_planes_device: full-resolution uint8 Y, Cr, Cb planes of an RGBA8
+ *     image (build_luminance_matrix / build_r,bChrominance_matrix,
+ *     JPEG.c:114-185), w*h bytes each.
+ *   jpegr_dct_blocks_device: discrete_cosine_transform (JPEG.c:451-494) of
+ *     nblocks planar uint8 blocks of `height` rows x `width` columns
+ *     (width 8 or 4, height 8), fp64 out, u*width+v order.
+ *   jpegr_quantize_device: Quantize (JPEG.c:621-629) in place on n doubles,
+ *     element i divided by table[i % size] (fp64 table) and truncated.
+ *   jpegr_permute_device: out[i] = in[(i/size)*size + perm[i%size]] for n
+ *     doubles (zigzag_pattern, JPEG.c:693-728, with perm = its scan order). */
+int jpegr_planes_device(const void *d_rgba, int w, int h, void *d_y, void *d_cr,
+                        void *d_cb, void *stream);
+int jpegr_dct_blocks_device(const void *d_blocks, int width, int height, int nblocks,
+                            void *d_out_f64, void *stream);
+int jpegr_quantize_device(void *d_coef_f64, const void *d_table_f64, int size,
+                          size_t n, void *stream);
+int jpegr_permute_device(const void *d_in_f64, void *d_out_f64, const void *d_perm_i32,
+                         int size, size_t n, void *stream);
+
 const char *jpegr_strerror(int code);
 
 #ifdef __cplusplus

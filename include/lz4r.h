@@ -98,6 +98,17 @@ int lz4r_copy_block_sizes(const lz4r_ctx *ctx, void *dst, size_t count,
 int lz4r_copy_block_offsets(const lz4r_ctx *ctx, void *dst, size_t count,
                             void *stream);
 
+/* Decode a framed stream (bytes as lz4r_compress writes them) back to the
+ * input.  Host C; replaces LZ4_decode / interpret_frame (LZ4.c:937-1121),
+ * which mis-parse streams of >= 256 blocks or literal runs >= 271: blocks are
+ * read until the input ends (the frame byte is checked modulo 256), literal
+ * lengths come from the exact u16 size field, and the format's one
+ * ambiguous token (a match of 257..259 stored as M = 1..3, LZ4.c:317) is
+ * resolved per block by backtracking.  LZ4R_ERR_CAPACITY sets *out_len to
+ * the length needed so far; LZ4R_ERR_CORRUPT on a malformed stream. */
+int lz4r_decompress(const uint8_t *in, size_t in_len, uint8_t *out, size_t cap,
+                    size_t *out_len);
+
 /* Host convenience wrapper around lz4r_compress_device (copies in and out). */
 int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
                   size_t *out_len);

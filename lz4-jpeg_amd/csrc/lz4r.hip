@@ -80,7 +80,6 @@ constexpr int kInOff = ((kTB * kBlkOutMax - (kTB - 1) * kBlk) + 15) / 16 * 16;
 constexpr int kRegion = kInOff + kTileIn + 48;  // + over-read pad (lcp, 32-B copy reads)
 constexpr int kHB = 9;                    // hash bits: 512 buckets
 constexpr int kH = 1 << kHB;
-constexpr uint32_t kEmpty = 0xFFFFFFFFu;  // position field 511 = none
 constexpr int kArr = kBlk + 4;
 
 static_assert((kTB - 1) * kBlk + kInOff >= kTB * kBlkOutMax, "output overlay bound");
@@ -92,11 +91,13 @@ constexpr uint64_t kValMask = (1ull << 38) - 1;
 
 struct TileLds {
   alignas(16) uint8_t buf[kRegion];
-  uint32_t head[kH];
-  uint32_t nxt[kArr];     // bucket cycles: entry of the next member
-  uint32_t rec[kArr];     // matchable p: M | dist<<8 | succ<<17
-  uint32_t seq[kArr];     // per sequence: cpos | end<<16; then pend | lit<<9
+  alignas(16) uint32_t cnt[kH + 4];  // bucket sizes, then bucket starts (+ total)
+  uint32_t srt[kArr];     // chain entries sorted by bucket
+  uint32_t rec[kArr];     // local(p) accumulator; then M | dist<<8 | succ<<17
+  uint32_t seq[kArr];     // candidate list; then per sequence: cpos | end<<16,
+                          // then pend | lit<<9
   uint16_t nm[kArr];      // first matchable position >= x
+  uint8_t vis[kArr];      // match starts visited by the greedy walk
   uint16_t bsize[kTB];
 };
 
@@ -216,70 +217,66 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
   const int lane = threadIdx.x;
   const int base = kInOff + k * kBlk;
 
-  // ---- index: chain every 4-gram start into its bucket --------------------
-  uint32_t key[5], ent[5], hb[5];
+  // ---- index: counting sort of the 4-gram starts by hash bucket -----------
+  // entry = position | preceding byte << 9 | 15-bit hash tag << 17; the
+  // bucket is the tag's top 9 bits, so equal tags imply equal buckets.
+  uint32_t key[5], ent[5], hb[5], slot[5];
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     const int p = r * 64 + lane;
     key[r] = p < n ? load4u(S.buf, base + p) : 0u;
     const uint32_t pb = p >= 1 && p < n ? (uint32_t)S.buf[base + p - 1] : 0u;
-    const uint32_t hm = key[r] * 2654435761u;
-    hb[r] = hm >> (32 - kHB);
-    ent[r] = (uint32_t)p | (pb << 9) | (((hm >> 8) & 0x7FFFu) << 17);
-  }
-  uint32_t old[5];
-#pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int p = r * 64 + lane;
-    old[r] = kEmpty;
+    const uint32_t tag = (key[r] * 2654435761u) >> 17;
+    hb[r] = tag >> (15 - kHB);
+    ent[r] = (uint32_t)p | (pb << 9) | (tag << 17);
     if (p < n) S.rec[p] = 0u;            // local(p) accumulator
-    if ((LZ4R_VARIANT < 2 || LZ4R_VARIANT == 4) && p + 4 <= n) {
-      old[r] = atomicExch(&S.head[hb[r]], ent[r]);
-      S.nxt[p] = old[r];
+  }
+  const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
+  const bool search = LZ4R_VARIANT == 0 || LZ4R_VARIANT == 4;
+  if (search) {
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int p = r * 64 + lane;
+      if (p < nk) slot[r] = atomicAdd(&S.cnt[hb[r]], 1u);
     }
   }
   __syncthreads();
-  uint32_t todo = 0;                     // rounds whose bucket has other members
+  if (search) {
+    // exclusive scan of the 512 bucket sizes: lane owns buckets 8l .. 8l+7
+    uint4 a = reinterpret_cast<const uint4 *>(S.cnt)[2 * lane];
+    uint4 b = reinterpret_cast<const uint4 *>(S.cnt)[2 * lane + 1];
+    const uint32_t tot = a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
+    uint32_t run = wave_incl_add(tot) - tot;
+    uint4 sa, sb;
+    sa.x = run; run += a.x; sa.y = run; run += a.y; sa.z = run; run += a.z; sa.w = run; run += a.w;
+    sb.x = run; run += b.x; sb.y = run; run += b.y; sb.z = run; run += b.z; sb.w = run; run += b.w;
+    reinterpret_cast<uint4 *>(S.cnt)[2 * lane] = sa;
+    reinterpret_cast<uint4 *>(S.cnt)[2 * lane + 1] = sb;
+    if (lane == 63) S.cnt[kH] = run;
+  }
+  __syncthreads();
+  if (search) {
 #pragma unroll
-  for (int r = 0; r < 5; ++r) {          // close each bucket list into a cycle
-    const int p = r * 64 + lane;
-    if (p + 4 <= n) {
-      bool alone = false;
-      if ((old[r] & 511u) == 511u) {
-        const uint32_t h = S.head[hb[r]];
-        S.nxt[p] = h;
-        alone = h == ent[r];
-      }
-      if (!alone) todo |= 1u << r;
+    for (int r = 0; r < 5; ++r) {
+      const int p = r * 64 + lane;
+      if (p < nk) S.srt[S.cnt[hb[r]] + slot[r]] = ent[r];
     }
   }
   __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 5; ++r) {          // head is not read again in this block
-    const int p = r * 64 + lane;
-    if (p + 4 <= n) S.head[hb[r]] = kEmpty;
-  }
-  if (LZ4R_VARIANT != 0 && LZ4R_VARIANT != 4) todo = 0;
 
   PROF_T(0);
-  // ---- local(p): left-maximal candidates -> list -> lcp -> atomicMax -------
-  // One cursor per lane walks the lane's non-singleton bucket cycles one
-  // after another (one LDS read per step); candidate pairs (p, j) go to a
-  // wave list in S.seq, drained by a balanced lcp pass.
+  // ---- candidates: every unordered pair inside a bucket segment, once -------
+  // Lane owns sorted entry s and meets every earlier entry of its segment
+  // (independent loads).  A pair is a candidate when the tags agree and the
+  // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]): (j, p) with
+  // p = the later position, j = the earlier.  Candidates go to a list in
+  // S.seq, drained by a balanced lcp pass with LDS atomicMax into S.rec.
   {
-    int r = todo ? __builtin_ctz(todo) : 5;
-    uint32_t me = 0, cur = 0;
-    auto pick = [&](int rr) {
-      return rr == 0 ? ent[0] : rr == 1 ? ent[1] : rr == 2 ? ent[2] : rr == 3 ? ent[3] : ent[4];
-    };
-    if (r < 5) {
-      me = pick(r);
-      cur = S.nxt[r * 64 + lane];
-    }
-    int cnt = 0;
+    constexpr int kTrash = kArr - 1;
+    int ncand = 0;
     auto drain = [&]() {
       __syncthreads();
-      for (int i = lane; i < cnt; i += 64) {
+      for (int i = lane; i < ncand; i += 64) {
         const uint32_t pr = S.seq[i];
         const int p = (int)(pr & 0xFFFFu), j = (int)(pr >> 16);
         const int l = lcp(S.buf, base + j, base + p, n - p);
@@ -287,39 +284,42 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
       }
       __syncthreads();
     };
-    // Branch-free body: every lane issues exactly one LDS read per step from
-    // an always-valid address; non-candidates write to the trash slot.
-    constexpr int kTrash = kArr - 1;
-    while (__ballot(r < 5)) {
-      const bool act = r < 5;
-      const int p = r * 64 + lane;
-      const int jp = (int)(cur & 511u);
-      const bool done = act && jp == p;
-      const uint32_t x = cur ^ me;
-      const bool cand = act && jp < p && (x >> 17) == 0 &&
-                        (jp == 0 || (x & (255u << 9)) != 0);
-      const uint64_t cm = __ballot(cand);
-      const int slot = cand ? cnt + __popcll(cm & lanemask_lt()) : kTrash;
-      S.seq[slot] = (uint32_t)p | ((uint32_t)jp << 16);
-      cnt += __popcll(cm);
-      const uint32_t todo2 = done ? (todo & ~(1u << r)) : todo;
-      const int rn = todo2 ? __builtin_ctz(todo2) : 5;
-      const int r2 = done ? rn : r;
-      todo = todo2;
-      me = done ? pick(r2) : me;
-      const int addr = done ? (r2 < 5 ? r2 * 64 + lane : lane) : (act ? jp : lane);
-      cur = S.nxt[addr];
-      r = r2;
-      if (cnt > kTrash - 64) {
-        drain();
-        cnt = 0;
+    for (int r = 0; search && r * 64 < nk; ++r) {
+      const int si = r * 64 + lane;
+      uint32_t me = 0;
+      int beg = 0, len = 0;
+      if (si < nk) {
+        me = S.srt[si];
+        beg = (int)S.cnt[(me >> 17) >> (15 - kHB)];
+        len = si - beg;                          // earlier entries of my segment
+      }
+      int it = 0;
+      while (__ballot(it < len)) {
+        const bool act = it < len;
+        const uint32_t o = act ? S.srt[beg + it] : 0u;
+        const uint32_t x = o ^ me;
+        const int pa = (int)(me & 511u), pj = (int)(o & 511u);
+        const int p = max(pa, pj), j = min(pa, pj);
+        const bool cand = act && (x >> 17) == 0 && (j == 0 || (x & (255u << 9)) != 0);
+        const uint64_t cm = __ballot(cand);
+        const int sl = cand ? ncand + __popcll(cm & lanemask_lt()) : kTrash;
+        S.seq[sl] = (uint32_t)p | ((uint32_t)j << 16);
+        ncand += __popcll(cm);
+        ++it;
+        if (ncand > kTrash - 64) {
+          drain();
+          ncand = 0;
+        }
       }
     }
-    PROF_T(1);
-    if (cnt) drain();
-    PROF_T(2);
+    if (ncand) drain();
+    // reset the bucket counters for the next block
+    reinterpret_cast<uint4 *>(S.cnt)[2 * lane] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4 *>(S.cnt)[2 * lane + 1] = make_uint4(0, 0, 0, 0);
   }
+  PROF_T(1);
   __syncthreads();
+  PROF_T(2);
   int bl[5], bj[5];
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
@@ -369,26 +369,26 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
 
   PROF_T(3);
   // ---- greedy parse = walk over match starts (LZ4.c:516-583) ---------------
-  uint64_t V0 = 0, V1 = 0, V2 = 0, V3 = 0, V4 = 0;      // visited match starts
   int c = F[0], e = 0, Sv = 0;
   while (c < n) {
     const uint32_t rv = __builtin_amdgcn_readfirstlane(S.rec[c]);
     e = c + (int)(rv & 255u);
-    if (lane == 0) S.seq[Sv] = (uint32_t)c | ((uint32_t)e << 16);
-    const uint64_t bit = 1ull << (c & 63);
-    switch (c >> 6) {
-      case 0: V0 |= bit; break;
-      case 1: V1 |= bit; break;
-      case 2: V2 |= bit; break;
-      case 3: V3 |= bit; break;
-      default: V4 |= bit; break;
+    if (lane == 0) {
+      S.seq[Sv] = (uint32_t)c | ((uint32_t)e << 16);
+      S.vis[c] = 1;
     }
     ++Sv;
     c = (int)(rv >> 17);
   }
-  const uint64_t V[5] = {V0, V1, V2, V3, V4};
   __syncthreads();
-
+  uint64_t V[5];
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int p = r * 64 + lane;
+    const bool v = p < n && S.vis[p] != 0;
+    V[r] = __ballot(v);
+    if (v) S.vis[p] = 0;
+  }
   PROF_T(4);
   // ---- sequences: lane kk = sequence kk ------------------------------------
   const int nseq = Sv + (e < n ? 1 : 0);
@@ -481,7 +481,8 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   uint64_t prof_last = 0;
 #endif
 
-  for (int i = lane; i < kH; i += 64) S.head[i] = kEmpty;
+  for (int i = lane; i < kH + 4; i += 64) S.cnt[i] = 0u;
+  for (int i = lane; i < kArr; i += 64) S.vis[i] = 0;
 
   for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const size_t b0 = t * kTB;

@@ -1,0 +1,104 @@
+/*
+ * JPEG_seq -- drop-in for the reference's JPEG_seq.exe
+ * (Algorithms/sequential/JPEG/JPEG.c main, :1099-1460) on the MI355X path.
+ *
+ * File contract (run from Experiment/, JPEG_sequential_experiment.c:99):
+ *   reads  ../Assets/Images/rand_8X8.png            (JPEG.c:9, :1102)
+ *   writes ../Output-Input/Images/original.png, luminance.png,
+ *          rChrominance.png, bChrominance.png       (JPEG.c:1105, :1121-1123)
+ *          ../Output-Input/Images/coefficients.bin  the quantised zigzag
+ *          coefficients: int16 LE per 8x8 tile [Y 64][Cr 32][Cb 32], tiles
+ *          in raster order (the reference keeps them in memory only)
+ *   exit 0; unreadable image: "Error loading image" and exit(1) (JPEG.c:74-78).
+ * Colour planes, DCT, quantisation and zigzag run on the GPU (jpegr_*).
+ * reconstructed.png (IDCT side, JPEG.c:1408-1423) is not produced yet.
+ * Optional argv[1] / argv[2] override the input image / output directory.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "../../include/jpegr.h"
+#include "lzj_host.h"
+
+#define IMAGES_DIRECTORY "../Assets/Images/"
+#define OUTPUT_DIRECTORY "../Output-Input/Images/"
+
+static void fail(const char *what) {
+  fprintf(stderr, "Error: %s\n", what);
+  exit(1);
+}
+
+static void write_png(const char *dir, const char *name, int w, int h, const uint8_t *rgba) {
+  char path[4096];
+  snprintf(path, sizeof path, "%s%s", dir, name);
+  if (lzj_png_write(path, w, h, rgba) != 0) printf("Error: Failed to write the PNG image.\n");
+}
+
+/* (uint8_t) of the reference's double expression: gcc/x86-64 truncates to
+ * int, then keeps the low byte (JPEG.c:234-236, 263-266, 288-291). */
+static uint8_t u8_of(double v) { return (uint8_t)(int)v; }
+
+int main(int argc, char **argv) {
+  const char *in_path = argc > 1 ? argv[1] : IMAGES_DIRECTORY "rand_8X8.png";
+  const char *out_dir = argc > 2 ? argv[2] : OUTPUT_DIRECTORY;
+  int w = 0, h = 0;
+  uint8_t *rgba = NULL;
+  if (lzj_png_read(in_path, &w, &h, &rgba) != 0) {
+    printf("Error loading image\n");
+    exit(1);
+  }
+  const size_t npx = (size_t)w * h;
+  const size_t ncoef = jpegr_coef_count(w, h);
+  void *d_rgba = NULL, *d_y = NULL, *d_cr = NULL, *d_cb = NULL, *d_coef = NULL;
+  if (hipMalloc(&d_rgba, npx * 4) != hipSuccess || hipMalloc(&d_y, npx) != hipSuccess ||
+      hipMalloc(&d_cr, npx) != hipSuccess || hipMalloc(&d_cb, npx) != hipSuccess ||
+      hipMalloc(&d_coef, ncoef * 2) != hipSuccess)
+    fail("device allocation failed");
+  if (hipMemcpy(d_rgba, rgba, npx * 4, hipMemcpyHostToDevice) != hipSuccess) fail("copy in");
+  if (jpegr_planes_device(d_rgba, w, h, d_y, d_cr, d_cb, NULL) != JPEGR_OK ||
+      jpegr_encode_device(d_rgba, w, h, 1, d_coef, NULL) != JPEGR_OK)
+    fail("kernel launch");
+  uint8_t *y = malloc(npx), *cr = malloc(npx), *cb = malloc(npx), *vis = malloc(npx * 4);
+  int16_t *coef = malloc(ncoef * 2);
+  if (!y || !cr || !cb || !vis || !coef) fail("out of memory");
+  if (hipMemcpy(y, d_y, npx, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(cr, d_cr, npx, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(cb, d_cb, npx, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(coef, d_coef, ncoef * 2, hipMemcpyDeviceToHost) != hipSuccess)
+    fail("copy out");
+
+  write_png(out_dir, "original.png", w, h, rgba);                    /* JPEG.c:1105 */
+  for (size_t i = 0; i < npx; ++i) {                                   /* JPEG.c:218-241 */
+    vis[4 * i] = vis[4 * i + 1] = vis[4 * i + 2] = y[i];
+    vis[4 * i + 3] = 255;
+  }
+  write_png(out_dir, "luminance.png", w, h, vis);
+  for (size_t i = 0; i < npx; ++i) {                                   /* JPEG.c:253-276 */
+    vis[4 * i] = u8_of(128 + 1.402 * (cr[i] - 128));
+    vis[4 * i + 1] = u8_of(128 - 0.344 * (128 - 128) - 0.714 * (cr[i] - 128));
+    vis[4 * i + 2] = u8_of(128 + 1.772 * (128 - 128));
+    vis[4 * i + 3] = 255;
+  }
+  write_png(out_dir, "rChrominance.png", w, h, vis);
+  for (size_t i = 0; i < npx; ++i) {                                   /* JPEG.c:278-300 */
+    vis[4 * i] = u8_of(128 + 1.402 * (128 - 128));
+    vis[4 * i + 1] = u8_of(128 - 0.344 * (cb[i] - 128) - 0.714 * (128 - 128));
+    vis[4 * i + 2] = u8_of(128 + 1.772 * (cb[i] - 128));
+    vis[4 * i + 3] = 255;
+  }
+  write_png(out_dir, "bChrominance.png", w, h, vis);
+
+  char path[4096];
+  snprintf(path, sizeof path, "%scoefficients.bin", out_dir);
+  FILE *f = fopen(path, "wb");
+  if (!f || fwrite(coef, 2, ncoef, f) != ncoef) fail("cannot write coefficients.bin");
+  fclose(f);
+  (void)hipFree(d_rgba); (void)hipFree(d_y); (void)hipFree(d_cr); (void)hipFree(d_cb);
+  (void)hipFree(d_coef);
+  free(rgba); free(y); free(cr); free(cb); free(vis); free(coef);
+  return 0;
+}

@@ -8,7 +8,7 @@
  * Reader: 8-bit, non-interlaced; colour types 0 (grey), 2 (RGB), 3 (palette),
  * 4 (grey+alpha), 6 (RGBA); all five row filters; output RGBA8 with the
  * reference's mapping (r,g,b from the first three channels, a = 255 when the
- * image has no alpha, JPEG.c:90-93).  Writer: RGBA8, filter 0, zlib level 6.
+ * image has no alpha, JPEG.c:90-93).  Writer: RGBA8, filter 0, zlib level 1.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -176,7 +176,7 @@ int lzj_png_write(const char *path, int w, int h, const uint8_t *rgba) {
     raw[y * (stride + 1)] = 0;
     memcpy(raw + y * (stride + 1) + 1, rgba + (size_t)y * stride, stride);
   }
-  if (compress2(z, &zlen, raw, (uLong)raw_len, 6) != Z_OK) goto out;
+  if (compress2(z, &zlen, raw, (uLong)raw_len, 1) != Z_OK) goto out;
   f = fopen(path, "wb");
   if (!f) goto out;
   uint8_t ihdr[13];

@@ -27,6 +27,7 @@ SIGNATURES = [
     ("lz4r_copy_block_sizes", _i, [_vp, _vp, _c_size, _vp]),
     ("lz4r_copy_block_offsets", _i, [_vp, _vp, _c_size, _vp]),
     ("lz4r_compress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
+    ("lz4r_decompress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
     ("lz4r_set_timing", _i, [_vp, _i]),
     ("lz4r_last_timing", _i, [_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ("lz4r_strerror", ctypes.c_char_p, [_i]),
@@ -36,11 +37,22 @@ SIGNATURES = [
     ("jpegr_dct_raw_device", _i, [_vp, _i, _i, _i, _vp, _vp]),
     ("jpegr_encode", _i, [_vp, _i, _i, _vp]),
     ("jpegr_time_device", _i, [_vp, _i, _i, _i, _vp, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
+    ("jpegr_planes_device", _i, [_vp, _i, _i, _vp, _vp, _vp, _vp]),
+    ("jpegr_dct_blocks_device", _i, [_vp, _i, _i, _i, _vp, _vp]),
+    ("jpegr_quantize_device", _i, [_vp, _vp, _i, _c_size, _vp]),
+    ("jpegr_permute_device", _i, [_vp, _vp, _vp, _i, _c_size, _vp]),
     ("jpegr_strerror", ctypes.c_char_p, [_i]),
     # lz4jpeg_synth.h
     ("lz4jpeg_rand_rgba", None, [ctypes.c_uint, _i, _i, _vp]),
     ("lz4jpeg_random_passages", _c_size, [_vp, _c_size, ctypes.c_uint, _c_size, _c_size, _c_size,
                                          _vp]),
+    # lz4jpeg_compat.h (the reference's own function names, on the GPU path)
+    ("lz4_encode", None, []),
+    ("LZ4_decode", None, [ctypes.c_char_p, ctypes.c_char_p]),
+    ("discrete_cosine_transform", None, [_vp, _c_size, _c_size, ctypes.POINTER(ctypes.POINTER(
+        ctypes.c_double))]),
+    ("Quantize", None, [ctypes.POINTER(ctypes.POINTER(ctypes.c_double)), _vp, _c_size]),
+    ("zigzag_pattern", None, [_c_size, _c_size, _vp, _vp]),
 ]
 
 _lib = None

@@ -142,3 +142,19 @@ def compress(data):
     if rc != 0:
         _raise(rc, "lz4r_compress")
     return out[:got.value].tobytes()
+
+
+def decompress(stream, cap=None):
+    """Exact host decoder (lz4r_decompress): framed stream bytes -> original
+    bytes.  Replaces LZ4_decode (LZ4.c:1038-1121); raises Lz4Error(-6) on a
+    malformed stream."""
+    buf = np.frombuffer(bytes(stream), dtype=np.uint8)
+    if cap is None:
+        cap = (buf.size // 5 + 1) * BLOCK
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    got = ctypes.c_size_t(0)
+    rc = _lib.lib().lz4r_decompress(buf.ctypes.data_as(ctypes.c_void_p), buf.size,
+                                    out.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(got))
+    if rc != 0:
+        _raise(rc, "lz4r_decompress")
+    return out[:got.value].tobytes()

@@ -10,7 +10,8 @@ import pytest
 from lz4jpeg import _lib
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(REPO, "include", h) for h in ("lz4r.h", "jpegr.h", "lz4jpeg_synth.h")]
+HEADERS = [os.path.join(REPO, "include", h)
+           for h in ("lz4r.h", "jpegr.h", "lz4jpeg_synth.h", "lz4jpeg_compat.h")]
 
 
 def declared_functions():

@@ -1,0 +1,81 @@
+"""The reference-named functions of include/lz4jpeg_compat.h (GPU-backed)
+give the reference's results: discrete_cosine_transform / Quantize /
+zigzag_pattern against the oracle's per-tile values, lz4_encode / LZ4_decode
+against the file contract."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import golden_inputs
+from lz4jpeg import _lib
+
+pytestmark = pytest.mark.gpu
+
+ZZ8 = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34,
+       27, 20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37,
+       44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63]
+ZZ4 = [0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 16, 13, 10, 7, 11, 14, 17, 20, 24, 21, 18, 15, 19, 22,
+       25, 28, 29, 26, 23, 27, 30, 31]
+LUMA_Q = [8, 6, 6, 8, 10, 14, 18, 22, 6, 6, 7, 9, 12, 20, 22, 20, 6, 7, 8, 10, 14, 22, 25, 22,
+          8, 9, 10, 14, 18, 28, 27, 22, 10, 12, 14, 18, 22, 35, 33, 26, 14, 18, 22, 22, 27, 33,
+          36, 30, 18, 22, 26, 28, 33, 40, 40, 34, 22, 26, 28, 30, 36, 34, 35, 33]
+
+
+def _dct(block_u8, width):
+    L = _lib.lib()
+    buf = np.ascontiguousarray(block_u8, dtype=np.uint8)
+    out = ctypes.POINTER(ctypes.c_double)()
+    L.discrete_cosine_transform(buf.ctypes.data_as(ctypes.c_void_p), width, 8, ctypes.byref(out))
+    res = np.array([out[i] for i in range(8 * width)])
+    ctypes.CDLL(None).free(out)
+    return res
+
+
+def test_dct_quant_zigzag_match_oracle(gpu, oracle):
+    w, h = 16, 8
+    img = oracle.rand_image(w, h, seed=11)
+    raw = oracle.jpeg_dct_raw(img).reshape(-1, 128)          # per tile [Y64][Cr32][Cb32]
+    coef = oracle.jpeg_encode(img).reshape(-1, 128)
+    y = np.empty((h, w), np.uint8)
+    cr = np.empty((h, w), np.uint8)
+    cb = np.empty((h, w), np.uint8)
+    oracle.L.jo_planes(np.ascontiguousarray(img).ctypes.data_as(ctypes.c_void_p), w, h,
+                       y.ctypes.data_as(ctypes.c_void_p), cr.ctypes.data_as(ctypes.c_void_p),
+                       cb.ctypes.data_as(ctypes.c_void_p))
+    L = _lib.lib()
+    for t in range(2):
+        yblk = y[:, 8 * t:8 * t + 8]
+        d = _dct(yblk, 8)
+        assert np.array_equal(d.view(np.uint64), raw[t, :64].view(np.uint64))   # bit-exact
+        crs = cr[:, 1::2][:, 4 * t:4 * t + 4]                 # odd columns (JPEG.c:329)
+        dc = _dct(crs, 4)
+        assert np.array_equal(dc.view(np.uint64), raw[t, 64:96].view(np.uint64))
+        # Quantize (JPEG.c:621) then zigzag (JPEG.c:693) == the fused kernel's tile
+        q = d.copy()
+        qp = ctypes.cast(q.ctypes.data, ctypes.POINTER(ctypes.c_double))
+        tab = np.array(LUMA_Q, dtype=np.uint64)
+        L.Quantize(ctypes.byref(qp), tab.ctypes.data_as(ctypes.c_void_p), 64)
+        assert np.array_equal(q, np.trunc(d / np.array(LUMA_Q, dtype=np.float64)))
+        zz = np.empty(64)
+        L.zigzag_pattern(8, 8, q.ctypes.data_as(ctypes.c_void_p), zz.ctypes.data_as(ctypes.c_void_p))
+        assert np.array_equal(zz, q[ZZ8])
+        assert np.array_equal(zz.astype(np.int16), coef[t, :64])
+        z4 = np.empty(32)
+        L.zigzag_pattern(4, 8, dc.ctypes.data_as(ctypes.c_void_p), z4.ctypes.data_as(ctypes.c_void_p))
+        assert np.array_equal(z4, dc[ZZ4])
+
+
+def test_lz4_encode_decode_file_contract(gpu, oracle, tmp_path, monkeypatch):
+    for d in ("Experiment", "Output-Input/input", "Output-Input/out", "Output-Input/log"):
+        os.makedirs(tmp_path / d, exist_ok=True)
+    data = golden_inputs.lz4_input("text_10000")
+    (tmp_path / "Output-Input/input/input.txt").write_bytes(data)
+    monkeypatch.chdir(tmp_path / "Experiment")
+    L = _lib.lib()
+    L.lz4_encode()
+    comp = (tmp_path / "Output-Input/out/compressed.bin").read_bytes()
+    assert comp == oracle.lz4_compress(data)
+    L.LZ4_decode(b"../Output-Input/out/compressed.bin", b"../Output-Input/log/encoding_log.txt")
+    assert (tmp_path / "Output-Input/out/uncompressed.txt").read_bytes() == data

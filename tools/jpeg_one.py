@@ -1,0 +1,17 @@
+"""Run the JPEG encoder a few times on one 3840x2160 random image (for profilers)."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "lz4-jpeg_amd")]
+import torch  # noqa: E402
+from lz4jpeg import jpeg, synth  # noqa: E402
+
+w, h = 3840, 2160
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+img = torch.from_numpy(synth.rand_rgba(w, h, seed=1)).cuda()
+out = torch.empty(jpeg.coef_count(w, h), dtype=torch.int16, device="cuda")
+for _ in range(reps):
+    jpeg.encode_device(img, w, h, 1, out)
+torch.cuda.synchronize()
+print("ok", flush=True)
