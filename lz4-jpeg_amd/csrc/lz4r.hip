@@ -5,20 +5,21 @@
 // in every block, greedily parses with an exhaustive longest-match search over
 // the whole block prefix (find_longest_match, LZ4.c:290-323; strict '>' so the
 // smallest i -- farthest offset -- wins ties; length truncated to uint8_t).
-// Blocks are independent, so the whole compressor is ONE single-pass kernel.
+// Blocks are independent; the compressor is one compute kernel plus a cheap
+// placement pass:
 //
-// lz4_tiles: persistent; workgroup = one wave; tiles of kTB = 8 consecutive
-// blocks (2,400 B) dealt round-robin to the resident waves.  Per tile:
-//   stage    tile bytes -> LDS (16-B loads: the only HBM read).
+// lz4_tiles: workgroup = one wave = one tile of kTB = 4 consecutive blocks
+// (1,200 B).  Per tile:
+//   stage    tile bytes -> LDS (16-B loads: the only read of the input).
 //   per block, position-parallel (lane owns p = 64r + lane, r < 5):
-//     index  every 4-gram start p is chained into its LDS hash bucket
-//            (atomic exchange; the bucket lists are closed into cycles, so
-//            the result does not depend on atomic order).  A chain entry is
-//            self-describing: position | preceding byte | 15-bit hash tag.
-//     local  each lane walks its 5 cycles interleaved (one LDS read per
-//            step) and measures only LEFT-MAXIMAL candidates j < p (equal
-//            4-gram, and j == 0 or blk[j-1] != blk[p-1]): the longest one,
-//            ties to the smallest j, is local(p).
+//     index  counting sort of the 4-gram starts by a 9-bit hash (LDS
+//            atomicAdd slot, DPP scan of the 512 bucket counts, scatter of
+//            self-describing entries pos | preceding byte << 9 | tag << 17).
+//     local  every unordered pair inside a bucket segment is met once
+//            (independent LDS loads); a pair (j < p) is a candidate when the
+//            tags agree and it is LEFT-MAXIMAL (j == 0 or blk[j-1] !=
+//            blk[p-1]); a balanced lcp pass takes the longest candidate per
+//            p, ties to the smallest j (LDS atomicMax).
 //     best   a candidate that is not left-maximal is the pair (j-1, p-1)
 //            shifted by one, whose match is one byte longer.  Hence
 //              best(p) = lexmax over q <= p of (q + local_len(q), q - local_j(q))
@@ -33,13 +34,13 @@
 //            size / literal-extension / offset bytes (write_sequence,
 //            LZ4.c:365-413), then a position-parallel literal scatter, into
 //            the tile's LDS output (overlaying already-consumed input).
-//   publish  decoupled look-back over tile byte counts (one 8-byte
-//            {epoch, flag, value} word per tile) -> tile's output offset.
-//   store    LDS -> HBM as aligned 16-B stores.
-// HBM traffic per input byte: 1 B read + ~1.03 B written (+2 B per block of
-// per-block sizes).  Forward progress of the look-back: every tile waits only
-// on lower tiles, each wave takes its tiles in increasing order and the grid
-// never exceeds the co-resident wave count (lz4r_ctx.max_grid).
+//   store    the tile's bytes -> its 16-B aligned scratch slot, size -> tsz.
+// lz4_scan_reduce / lz4_scan_partials: exclusive scan of tile sizes.
+// lz4_gather: 64 tiles per workgroup, slot -> final offset, 16-B stores.
+// No workgroup ever waits on another (a fused decoupled look-back ran the
+// waves in lock-step at the pace of the slowest tile of each round).
+// HBM traffic per input byte: 1 B read + ~1.03 B written by lz4_tiles, and
+// ~1.03 B read + ~1.03 B written by lz4_gather (+2 B/block of block sizes).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -49,8 +50,7 @@
 #include "../../include/lz4r.h"
 
 // LZ4R_VARIANT (timing ablations only, never shipped): 1 = no match search,
-// 2 = no index/match phase, 3 = 2 + no look-back (fixed output slots),
-// 4 = full search, no look-back
+// 2 = no index/match phase
 #ifndef LZ4R_VARIANT
 #define LZ4R_VARIANT 0
 #endif
@@ -70,7 +70,7 @@ __device__ __forceinline__ uint64_t prof_now() {
 namespace {
 
 constexpr int kBlk = LZ4R_BLOCK;          // 300
-constexpr int kTB = 8;                    // blocks per tile
+constexpr int kTB = 4;                    // blocks per tile
 constexpr int kTileIn = kTB * kBlk;       // 2400 B, multiple of 16
 constexpr int kBlkOutMax = 600;           // >= 548: worst-case bytes of one block
 // The tile's output grows from buf[0]; block k's input sits at
@@ -85,9 +85,8 @@ constexpr int kArr = kBlk + 4;
 static_assert((kTB - 1) * kBlk + kInOff >= kTB * kBlkOutMax, "output overlay bound");
 static_assert(kInOff % 16 == 0 && kTileIn % 16 == 0, "16-B staging");
 
-// status word of a tile: epoch[63:40] | flag[39:38] | value[37:0]
-constexpr uint64_t kFlagAgg = 1, kFlagPre = 2;
-constexpr uint64_t kValMask = (1ull << 38) - 1;
+constexpr int kSlot = kTB * kBlkOutMax;   // scratch bytes per tile (16-B multiple)
+static_assert(kSlot % 16 == 0, "aligned slots");
 
 struct TileLds {
   alignas(16) uint8_t buf[kRegion];
@@ -202,12 +201,6 @@ __device__ __forceinline__ uint4 funnel16(uint4 lo, uint4 hi, int sb) {
                     __builtin_amdgcn_alignbyte(x[4], x[3], by));
 }
 
-__device__ __forceinline__ uint64_t status_load(const uint64_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void status_store(uint64_t *p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Encode block `k` of the tile (n bytes at S.buf[kInOff + 300k]) into
 // S.buf[obase ...]; returns the bytes written.
@@ -470,8 +463,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
 
 __global__ __launch_bounds__(64) void lz4_tiles(
     const uint8_t *__restrict__ in, size_t n_total, size_t nb_total, size_t ntiles,
-    uint8_t *__restrict__ out, uint64_t cap, int hdr, uint64_t *__restrict__ d_len,
-    uint16_t *__restrict__ bsizes, uint64_t *__restrict__ status, uint64_t epoch) {
+    uint8_t *__restrict__ slots, uint32_t *__restrict__ tsz,
+    uint16_t *__restrict__ bsizes) {
   __shared__ TileLds S;
   const int lane = threadIdx.x;
   uint64_t prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -515,67 +508,14 @@ __global__ __launch_bounds__(64) void lz4_tiles(
     __syncthreads();
     if (lane < nbt) bsizes[b0 + lane] = S.bsize[lane];
 
-    PROF_T(7);
-    // ---- decoupled look-back: exclusive byte offset of this tile ------------
-    const uint64_t agg = (uint64_t)obase;
-    const uint64_t ep = epoch << 40;
-    uint64_t excl = 0;
-    if (LZ4R_VARIANT >= 3) {
-      excl = t * (uint64_t)kTB * kBlkOutMax;
-    } else if (t == 0) {
-      if (lane == 0) status_store(&status[0], ep | (kFlagPre << 38) | agg);
-    } else {
-      if (lane == 0) status_store(&status[t], ep | (kFlagAgg << 38) | agg);
-      long long j = (long long)t - 1;               // closest predecessor not yet summed
-      while (true) {
-        const long long idx = j - lane;
-        uint64_t s = ep | (kFlagPre << 38);         // before tile 0: prefix 0
-        if (idx >= 0) s = status_load(&status[idx]);
-        const bool ready = (s >> 40) == epoch && ((s >> 38) & 3u) != 0;
-        const bool pre = ready && ((s >> 38) & 3u) == kFlagPre;
-        const uint64_t pmask = __ballot(pre);
-        const uint64_t nready = __ballot(!ready);
-        const int fp = pmask ? ctz64(pmask) : 64;   // nearest inclusive prefix
-        const uint64_t need = fp >= 63 ? ~0ull : ((2ull << fp) - 1ull);
-        if (nready & need) {                        // a needed predecessor is not out yet
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        const uint64_t v = (lane <= fp) ? (s & kValMask) : 0;
-        excl += wave_sum64(v);
-        if (fp < 64) break;
-        j -= 64;
-      }
-      if (lane == 0) status_store(&status[t], ep | (kFlagPre << 38) | ((excl + agg) & kValMask));
-    }
-    if (t == ntiles - 1 && lane == 0) *d_len = (uint64_t)hdr + excl + agg;
-    if (hdr && t == 0 && lane == 0 && cap > 0) out[0] = (uint8_t)nb_total;   // LZ4.c:429
-
     PROF_T(8);
-    // ---- store: LDS -> HBM as aligned 16-B chunks ----------------------------
-    const uint64_t o0 = (uint64_t)hdr + excl;
-    const uint64_t o1 = min(o0 + agg, cap);
-    if (o1 > o0) {
-      const uintptr_t abs0 = (uintptr_t)(out + o0);
-      const uintptr_t first = abs0 & ~(uintptr_t)15;
-      const uintptr_t absend = (uintptr_t)(out + o1);
-      const int shift = (int)(abs0 - first);        // uniform: 0..15
-      const int nchunks = (int)((absend - first + 15) >> 4);
-      for (int ci = lane; ci < nchunks; ci += 64) {
-        const uintptr_t a = first + ((uintptr_t)ci << 4);
-        const int s = ci * 16 - shift;              // LDS byte of chunk start
-        if (a >= abs0 && a + 16 <= absend) {
-          // bytes s .. s+15 lie in the 32 B at s & ~15; s & 15 is uniform
-          const uint4 *q = reinterpret_cast<const uint4 *>(S.buf + (s & ~15));
-          const uint4 lo = q[0], hi = q[1];
-          *reinterpret_cast<uint4 *>(a) = funnel16(lo, hi, s & 15);
-        } else {
-          for (int b = 0; b < 16; ++b) {
-            const uintptr_t ab = a + b;
-            if (ab >= abs0 && ab < absend) *reinterpret_cast<uint8_t *>(ab) = S.buf[s + b];
-          }
-        }
-      }
+    // ---- store: the tile's bytes to its 16-B aligned scratch slot ----------
+    {
+      uint4 *dst = reinterpret_cast<uint4 *>(slots + t * (size_t)kSlot);
+      const int nchunks = (obase + 15) >> 4;
+      for (int ci = lane; ci < nchunks; ci += 64)
+        dst[ci] = reinterpret_cast<const uint4 *>(S.buf)[ci];
+      if (lane == 0) tsz[t] = (uint32_t)obase;
     }
     __syncthreads();                                // LDS reused by the next tile
     PROF_T(9);
@@ -586,6 +526,110 @@ __global__ __launch_bounds__(64) void lz4_tiles(
 #endif
 }
 
+// ---- placement: exclusive scan of tile sizes, then gather -----------------
+constexpr int kPart = 4096;          // tiles per scan partial
+constexpr int kGT = 64;              // tiles per gather workgroup (256 threads)
+
+__global__ __launch_bounds__(256) void lz4_scan_reduce(const uint32_t *__restrict__ tsz,
+                                                       size_t ntiles,
+                                                       uint64_t *__restrict__ part) {
+  __shared__ uint64_t ws[4];
+  const size_t t0 = (size_t)blockIdx.x * kPart;
+  uint64_t s = 0;
+  for (int k = threadIdx.x; k < kPart; k += 256) {
+    const size_t i = t0 + k;
+    if (i < ntiles) s += tsz[i];
+  }
+  s = wave_sum64(s);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// one workgroup: exclusive scan of the partials in place; total -> *len
+__global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__ part,
+                                                          size_t nparts, uint64_t hdr,
+                                                          uint64_t *__restrict__ len) {
+  __shared__ uint64_t ws[16];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (size_t c0 = 0; c0 < nparts; c0 += 1024) {
+    const size_t i = c0 + threadIdx.x;
+    const uint64_t v = i < nparts ? part[i] : 0;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t o = __shfl_up(x, d, 64);
+      if ((threadIdx.x & 63) >= d) x += o;
+    }
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint64_t pre = carry;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) pre += ws[w];
+    if (i < nparts) part[i] = pre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = pre + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *len = hdr + carry;
+}
+
+// Workgroup = 64 consecutive tiles: offsets from the partials + a wave scan,
+// then each wave copies 16 tiles, slot -> out, as 16-B stores (bytes of
+// seam chunks individually).  Writes the frame byte (LZ4.c:429).
+__global__ __launch_bounds__(256) void lz4_gather(
+    const uint8_t *__restrict__ slots, const uint32_t *__restrict__ tsz, size_t ntiles,
+    const uint64_t *__restrict__ part, uint8_t *__restrict__ out, uint64_t cap, int hdr,
+    uint64_t nb_total) {
+  __shared__ uint64_t ws[4];
+  __shared__ uint64_t toff[kGT];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const size_t g0 = (size_t)blockIdx.x * kGT;
+  const size_t p = g0 / kPart;
+  // sizes of tiles [p*kPart, g0): 256 threads, <= 16 each
+  uint64_t s = 0;
+  for (size_t i = p * kPart + tid; i < g0; i += 256) s += tsz[i];
+  s = wave_sum64(s);
+  if (lane == 0) ws[wv] = s;
+  __syncthreads();
+  if (wv == 0) {
+    const uint64_t base = part[p] + ws[0] + ws[1] + ws[2] + ws[3] + (uint64_t)hdr;
+    const size_t t = g0 + lane;
+    const uint32_t v = t < ntiles ? tsz[t] : 0u;
+    const uint32_t inc = wave_incl_add(v);       // < 64 * 2400, fits 32 bits
+    toff[lane] = base + inc - v;
+  }
+  __syncthreads();
+  if (hdr && g0 == 0 && tid == 0 && cap > 0) out[0] = (uint8_t)nb_total;
+  for (int k = wv; k < kGT; k += 4) {
+    const size_t t = g0 + k;
+    if (t >= ntiles) break;
+    const uint64_t o0 = toff[k];
+    const uint64_t o1 = min(o0 + tsz[t], cap);
+    if (o1 <= o0) continue;
+    const uint8_t *src = slots + t * (size_t)kSlot;
+    const uintptr_t abs0 = (uintptr_t)(out + o0);
+    const uintptr_t first = abs0 & ~(uintptr_t)15;
+    const uintptr_t absend = (uintptr_t)(out + o1);
+    const int shift = (int)(abs0 - first);
+    const int nchunks = (int)((absend - first + 15) >> 4);
+    for (int ci = lane; ci < nchunks; ci += 64) {
+      const uintptr_t a = first + ((uintptr_t)ci << 4);
+      const int sb = ci * 16 - shift;               // source byte of chunk start
+      if (a >= abs0 && a + 16 <= absend) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(src + (sb & ~15));
+        *reinterpret_cast<uint4 *>(a) = funnel16(q[0], q[1], sb & 15);
+      } else {
+        for (int b = 0; b < 16; ++b) {
+          const uintptr_t ab = a + b;
+          if (ab >= abs0 && ab < absend) *reinterpret_cast<uint8_t *>(ab) = src[sb + b];
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 struct lz4r_ctx {
@@ -593,9 +637,10 @@ struct lz4r_ctx {
   size_t cap_blocks = 0;       // capacity of the per-block arrays
   size_t cap_tiles = 0;
   uint16_t *bsizes = nullptr;  // encoded bytes of every block of the last call
-  uint64_t *status = nullptr;  // look-back words, one per tile
-  uint64_t epoch = 0;
-  unsigned max_grid = 0;       // co-resident workgroups of lz4_tiles on this device
+  uint8_t *slots = nullptr;    // per-tile output slots (kSlot bytes each)
+  uint32_t *tsz = nullptr;     // encoded bytes per tile
+  uint64_t *part = nullptr;    // scan partials, one per kPart tiles
+  unsigned max_grid = 0;       // resident workgroups of lz4_tiles on this device
   uint64_t *len = nullptr;     // default device length slot
   size_t last_nb = 0;
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr;
@@ -607,9 +652,13 @@ namespace {
 
 void free_scratch(lz4r_ctx *c) {
   (void)hipFree(c->bsizes);
-  (void)hipFree(c->status);
+  (void)hipFree(c->slots);
+  (void)hipFree(c->tsz);
+  (void)hipFree(c->part);
   c->bsizes = nullptr;
-  c->status = nullptr;
+  c->slots = nullptr;
+  c->tsz = nullptr;
+  c->part = nullptr;
   c->cap_blocks = 0;
   c->cap_tiles = 0;
 }
@@ -619,13 +668,14 @@ int ensure_scratch(lz4r_ctx *c, size_t nb) {
   free_scratch(c);
   const size_t cap = nb + nb / 8 + 1024;
   const size_t tiles = (cap + kTB - 1) / kTB;
+  const size_t parts = (tiles + kPart - 1) / kPart;
   if (hipMalloc(&c->bsizes, cap * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&c->status, tiles * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(c->status, 0, tiles * sizeof(uint64_t)) != hipSuccess) {
+      hipMalloc(&c->slots, tiles * (size_t)kSlot) != hipSuccess ||
+      hipMalloc(&c->tsz, tiles * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&c->part, parts * sizeof(uint64_t)) != hipSuccess) {
     free_scratch(c);
     return LZ4R_ERR_NOMEM;
   }
-  c->epoch = 0;                // fresh (zeroed) status words: epochs restart
   c->cap_blocks = cap;
   c->cap_tiles = tiles;
   return LZ4R_OK;
@@ -642,23 +692,24 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   const size_t ntiles = (nb + kTB - 1) / kTB;
   if (ntiles > 0xffffffffULL || n > (1ull << 37)) return LZ4R_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (++c->epoch >= (1ull << 24)) {                 // epoch wrap: clear the words
-    if (hipMemsetAsync(c->status, 0, c->cap_tiles * sizeof(uint64_t), s) != hipSuccess)
-      return LZ4R_ERR_HIP;
-    c->epoch = 1;
-  }
   const bool timed = c->timing;
   c->timed_call = timed;
   if (timed) (void)hipEventRecord(c->ev_a, s);
-  const unsigned grid = (unsigned)(ntiles < c->max_grid ? ntiles : c->max_grid);
-  hipLaunchKernelGGL(lz4_tiles, dim3(grid), dim3(64), 0, s,
-                     static_cast<const uint8_t *>(d_in), n, nb, ntiles,
-                     static_cast<uint8_t *>(d_out), (uint64_t)cap, hdr,
-                     static_cast<uint64_t *>(d_len), c->bsizes, c->status, c->epoch);
-  if (timed) {
-    (void)hipEventRecord(c->ev_b, s);
-    (void)hipEventRecord(c->ev_c, s);
-  }
+  // one tile per workgroup: the hardware dispatcher balances the uneven
+  // per-tile cost (a static grid-stride split leaves a tail)
+  hipLaunchKernelGGL(lz4_tiles, dim3((unsigned)ntiles), dim3(64), 0, s,
+                     static_cast<const uint8_t *>(d_in), n, nb, ntiles, c->slots, c->tsz,
+                     c->bsizes);
+  if (timed) (void)hipEventRecord(c->ev_b, s);
+  const size_t nparts = (ntiles + kPart - 1) / kPart;
+  hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)nparts), dim3(256), 0, s, c->tsz, ntiles,
+                     c->part);
+  hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part, nparts,
+                     (uint64_t)hdr, static_cast<uint64_t *>(d_len));
+  hipLaunchKernelGGL(lz4_gather, dim3((unsigned)((ntiles + kGT - 1) / kGT)), dim3(256), 0, s,
+                     c->slots, c->tsz, ntiles, c->part, static_cast<uint8_t *>(d_out),
+                     (uint64_t)cap, hdr, (uint64_t)nb);
+  if (timed) (void)hipEventRecord(c->ev_c, s);
   c->last_nb = nb;
   return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
 }
@@ -689,11 +740,8 @@ int lz4r_ctx_create(lz4r_ctx **out) {
     lz4r_ctx_destroy(c);
     return LZ4R_ERR_HIP;
   }
-  // The look-back needs every workgroup of the grid resident at once (a tile
-  // waits on lower tiles only; each workgroup walks its tiles in order).
-  // One workgroup per CU of margin under the occupancy answer.
-  const int per_cu = occ > 1 ? occ - 1 : 1;
-  c->max_grid = (unsigned)(per_cu * cus);
+  // one resident wave per LDS/VGPR slot; tiles are taken grid-stride
+  c->max_grid = (unsigned)(occ * cus);
   *out = c;
   return LZ4R_OK;
 }
