@@ -90,15 +90,23 @@ static_assert(kSlot % 16 == 0, "aligned slots");
 
 struct TileLds {
   alignas(16) uint8_t buf[kRegion];
-  alignas(16) uint32_t cnt[kH + 4];  // bucket sizes, then bucket starts (+ total)
-  uint32_t srt[kArr];     // chain entries sorted by bucket
+  // two u16 bucket counters per word, then the bucket starts; afterwards the
+  // visit bytes of the greedy walk (all zero again when the block is done)
+  alignas(16) uint32_t cnt[kH / 2];
+  union {
+    uint32_t srt[kArr];   // entries sorted by bucket
+    uint16_t nm[kArr];    // then: first matchable position >= x
+  };
   uint32_t rec[kArr];     // local(p) accumulator; then M | dist<<8 | succ<<17
   uint32_t seq[kArr];     // candidate list; then per sequence: cpos | end<<16,
                           // then pend | lit<<9
-  uint16_t nm[kArr];      // first matchable position >= x
-  uint8_t vis[kArr];      // match starts visited by the greedy walk
   uint16_t bsize[kTB];
 };
+static_assert(kH / 2 * 4 >= kArr, "visit bytes fit in the counter words");
+
+__device__ __forceinline__ uint32_t bucket_start(const TileLds &S, uint32_t b) {
+  return (S.cnt[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu;
+}
 
 __device__ __forceinline__ uint32_t load4u(const uint8_t *b, int off) {
   const uint32_t *d = reinterpret_cast<const uint32_t *>(b);
@@ -230,29 +238,38 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = r * 64 + lane;
-      if (p < nk) slot[r] = atomicAdd(&S.cnt[hb[r]], 1u);
+      if (p < nk) {
+        const uint32_t sh = (hb[r] & 1u) * 16;
+        slot[r] = (atomicAdd(&S.cnt[hb[r] >> 1], 1u << sh) >> sh) & 0xFFFFu;
+      }
     }
   }
   __syncthreads();
   if (search) {
     // exclusive scan of the 512 bucket sizes: lane owns buckets 8l .. 8l+7
-    uint4 a = reinterpret_cast<const uint4 *>(S.cnt)[2 * lane];
-    uint4 b = reinterpret_cast<const uint4 *>(S.cnt)[2 * lane + 1];
-    const uint32_t tot = a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
+    // (words 4l .. 4l+3, two u16 counters each; starts <= 297 fit in u16)
+    const uint4 a = reinterpret_cast<const uint4 *>(S.cnt)[lane];
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+    uint32_t tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tot += (w[i] & 0xFFFFu) + (w[i] >> 16);
     uint32_t run = wave_incl_add(tot) - tot;
-    uint4 sa, sb;
-    sa.x = run; run += a.x; sa.y = run; run += a.y; sa.z = run; run += a.z; sa.w = run; run += a.w;
-    sb.x = run; run += b.x; sb.y = run; run += b.y; sb.z = run; run += b.z; sb.w = run; run += b.w;
-    reinterpret_cast<uint4 *>(S.cnt)[2 * lane] = sa;
-    reinterpret_cast<uint4 *>(S.cnt)[2 * lane + 1] = sb;
-    if (lane == 63) S.cnt[kH] = run;
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t lo = run;
+      run += w[i] & 0xFFFFu;
+      o[i] = lo | (run << 16);
+      run += w[i] >> 16;
+    }
+    reinterpret_cast<uint4 *>(S.cnt)[lane] = make_uint4(o[0], o[1], o[2], o[3]);
   }
   __syncthreads();
   if (search) {
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = r * 64 + lane;
-      if (p < nk) S.srt[S.cnt[hb[r]] + slot[r]] = ent[r];
+      if (p < nk) S.srt[bucket_start(S, hb[r]) + slot[r]] = ent[r];
     }
   }
   __syncthreads();
@@ -277,29 +294,47 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
       }
       __syncthreads();
     };
-    for (int r = 0; search && r * 64 < nk; ++r) {
+    // the five rounds' entries and segment starts are loaded up front
+    uint32_t meR[5];
+    int begR[5], lenR[5];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
       const int si = r * 64 + lane;
-      uint32_t me = 0;
-      int beg = 0, len = 0;
-      if (si < nk) {
-        me = S.srt[si];
-        beg = (int)S.cnt[(me >> 17) >> (15 - kHB)];
-        len = si - beg;                          // earlier entries of my segment
+      meR[r] = search && si < nk ? S.srt[si] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int si = r * 64 + lane;
+      begR[r] = 0;
+      lenR[r] = 0;
+      if (search && si < nk) {
+        begR[r] = (int)bucket_start(S, (meR[r] >> 17) >> (15 - kHB));
+        lenR[r] = si - begR[r];                  // earlier entries of my segment
       }
-      int it = 0;
-      while (__ballot(it < len)) {
-        const bool act = it < len;
-        const uint32_t o = act ? S.srt[beg + it] : 0u;
-        const uint32_t x = o ^ me;
-        const int pa = (int)(me & 511u), pj = (int)(o & 511u);
-        const int p = max(pa, pj), j = min(pa, pj);
-        const bool cand = act && (x >> 17) == 0 && (j == 0 || (x & (255u << 9)) != 0);
-        const uint64_t cm = __ballot(cand);
-        const int sl = cand ? ncand + __popcll(cm & lanemask_lt()) : kTrash;
-        S.seq[sl] = (uint32_t)p | ((uint32_t)j << 16);
-        ncand += __popcll(cm);
-        ++it;
-        if (ncand > kTrash - 64) {
+    }
+    auto pair = [&](uint32_t me, uint32_t o, bool act) {
+      const uint32_t x = o ^ me;
+      const int pa = (int)(me & 511u), pj = (int)(o & 511u);
+      const int p = max(pa, pj), j = min(pa, pj);
+      const bool cand = act && (x >> 17) == 0 && (j == 0 || (x & (255u << 9)) != 0);
+      const uint64_t cm = __ballot(cand);
+      const int sl = cand ? ncand + __popcll(cm & lanemask_lt()) : kTrash;
+      S.seq[sl] = (uint32_t)p | ((uint32_t)j << 16);
+      ncand += __popcll(cm);
+    };
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      if (r * 64 >= nk) break;
+      const uint32_t me = meR[r];
+      const int beg = begR[r], len = lenR[r];
+      // two members per step: independent loads, one latency
+      for (int it = 0; __ballot(it < len); it += 2) {
+        const bool a0 = it < len, a1 = it + 1 < len;
+        const uint32_t o0 = a0 ? S.srt[beg + it] : 0u;
+        const uint32_t o1 = a1 ? S.srt[beg + it + 1] : 0u;
+        pair(me, o0, a0);
+        pair(me, o1, a1);
+        if (ncand > kTrash - 128) {
           drain();
           ncand = 0;
         }
@@ -307,8 +342,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
     }
     if (ncand) drain();
     // reset the bucket counters for the next block
-    reinterpret_cast<uint4 *>(S.cnt)[2 * lane] = make_uint4(0, 0, 0, 0);
-    reinterpret_cast<uint4 *>(S.cnt)[2 * lane + 1] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4 *>(S.cnt)[lane] = make_uint4(0, 0, 0, 0);
   }
   PROF_T(1);
   __syncthreads();
@@ -368,7 +402,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
     e = c + (int)(rv & 255u);
     if (lane == 0) {
       S.seq[Sv] = (uint32_t)c | ((uint32_t)e << 16);
-      S.vis[c] = 1;
+      reinterpret_cast<uint8_t *>(S.cnt)[c] = 1;
     }
     ++Sv;
     c = (int)(rv >> 17);
@@ -378,9 +412,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     const int p = r * 64 + lane;
-    const bool v = p < n && S.vis[p] != 0;
+    uint8_t *vis = reinterpret_cast<uint8_t *>(S.cnt);
+    const bool v = p < n && vis[p] != 0;
     V[r] = __ballot(v);
-    if (v) S.vis[p] = 0;
+    if (v) vis[p] = 0;
   }
   PROF_T(4);
   // ---- sequences: lane kk = sequence kk ------------------------------------
@@ -474,8 +509,7 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   uint64_t prof_last = 0;
 #endif
 
-  for (int i = lane; i < kH + 4; i += 64) S.cnt[i] = 0u;
-  for (int i = lane; i < kArr; i += 64) S.vis[i] = 0;
+  for (int i = lane; i < kH / 2; i += 64) S.cnt[i] = 0u;
 
   for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const size_t b0 = t * kTB;
