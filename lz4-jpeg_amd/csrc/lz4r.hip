@@ -561,23 +561,32 @@ __global__ __launch_bounds__(64) void lz4_tiles(
 }
 
 // ---- placement: exclusive scan of tile sizes, then gather -----------------
-constexpr int kPart = 4096;          // tiles per scan partial
-constexpr int kGT = 64;              // tiles per gather workgroup (256 threads)
+constexpr int kGT = 64;              // tiles per gather group (one workgroup)
+constexpr int kPart = 64 * kGT;      // tiles per scan partial (64 groups)
 
+// per group of 64 tiles: gsum; per 64 groups: part
 __global__ __launch_bounds__(256) void lz4_scan_reduce(const uint32_t *__restrict__ tsz,
                                                        size_t ntiles,
+                                                       uint32_t *__restrict__ gsum,
                                                        uint64_t *__restrict__ part) {
   __shared__ uint64_t ws[4];
-  const size_t t0 = (size_t)blockIdx.x * kPart;
-  uint64_t s = 0;
-  for (int k = threadIdx.x; k < kPart; k += 256) {
+  const int tid = threadIdx.x;
+  const size_t t0 = (size_t)blockIdx.x * kPart + (size_t)tid * 16;   // 16 tiles per thread
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
     const size_t i = t0 + k;
-    if (i < ntiles) s += tsz[i];
+    if (i < ntiles) v += tsz[i];
   }
-  s = wave_sum64(s);
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);                      // 4 threads = one group of 64 tiles
+  const size_t g = (size_t)blockIdx.x * 64 + (tid >> 2);
+  if ((tid & 3) == 0 && g * kGT < ntiles) gsum[g] = v;
+  uint64_t w = (tid & 3) == 0 ? v : 0;
+  w = wave_sum64(w);
+  if ((tid & 63) == 0) ws[tid >> 6] = w;
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+  if (tid == 0) part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
 // one workgroup: exclusive scan of the partials in place; total -> *len
@@ -609,56 +618,81 @@ __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__
   if (threadIdx.x == 0) *len = hdr + carry;
 }
 
-// Workgroup = 64 consecutive tiles: offsets from the partials + a wave scan,
-// then each wave copies 16 tiles, slot -> out, as 16-B stores (bytes of
-// seam chunks individually).  Writes the frame byte (LZ4.c:429).
+// 16 bytes starting at byte `off` of a slot (off may be -15 .. slot size;
+// slots are preceded by a 16-B pad, so the aligned loads stay in bounds)
+__device__ __forceinline__ uint4 load16(const uint8_t *slot, long off) {
+  const long a = off & ~15L;
+  const uint4 *q = reinterpret_cast<const uint4 *>(slot + a);
+  return funnel16(q[0], q[1], (int)(off - a));
+}
+
+__device__ __forceinline__ uint4 select16(uint4 x, uint4 y, int k) {
+  // bytes < k from x, the rest from y (0 <= k <= 16)
+  uint32_t xv[4] = {x.x, x.y, x.z, x.w}, yv[4] = {y.x, y.y, y.z, y.w}, o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int lo = k - 4 * i;                     // bytes of this dword from x
+    const uint32_t m = lo <= 0 ? 0u : (lo >= 4 ? ~0u : ((1u << (8 * lo)) - 1u));
+    o[i] = (xv[i] & m) | (yv[i] & ~m);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// Workgroup = group of 64 consecutive tiles.  Offsets from the partials,
+// the group sums and a wave scan; then the group's output range is written
+// as aligned 16-B chunks, each assembled from at most two tiles' slots (a
+// tile is >= 32 B except the globally last).  Only the group's two edge
+// chunks are written bytewise.  Also writes the frame byte (LZ4.c:429).
 __global__ __launch_bounds__(256) void lz4_gather(
     const uint8_t *__restrict__ slots, const uint32_t *__restrict__ tsz, size_t ntiles,
-    const uint64_t *__restrict__ part, uint8_t *__restrict__ out, uint64_t cap, int hdr,
-    uint64_t nb_total) {
-  __shared__ uint64_t ws[4];
-  __shared__ uint64_t toff[kGT];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const size_t g0 = (size_t)blockIdx.x * kGT;
-  const size_t p = g0 / kPart;
-  // sizes of tiles [p*kPart, g0): 256 threads, <= 16 each
-  uint64_t s = 0;
-  for (size_t i = p * kPart + tid; i < g0; i += 256) s += tsz[i];
-  s = wave_sum64(s);
-  if (lane == 0) ws[wv] = s;
-  __syncthreads();
-  if (wv == 0) {
-    const uint64_t base = part[p] + ws[0] + ws[1] + ws[2] + ws[3] + (uint64_t)hdr;
-    const size_t t = g0 + lane;
-    const uint32_t v = t < ntiles ? tsz[t] : 0u;
-    const uint32_t inc = wave_incl_add(v);       // < 64 * 2400, fits 32 bits
-    toff[lane] = base + inc - v;
+    const uint32_t *__restrict__ gsum, const uint64_t *__restrict__ part,
+    uint8_t *__restrict__ out, uint64_t cap, int hdr, uint64_t nb_total) {
+  __shared__ uint64_t toff[kGT + 1];
+  const int tid = threadIdx.x;
+  const size_t g = blockIdx.x;
+  const size_t g0 = g * kGT;
+  const int nt = (int)min((size_t)kGT, ntiles - g0);
+  if (tid < 64) {
+    const size_t p = g0 / kPart;
+    const size_t gfirst = p * 64;                  // first group of the partial
+    uint64_t s = (gfirst + tid < g) ? gsum[gfirst + tid] : 0u;
+    s = wave_sum64(s);
+    const uint64_t base = part[p] + s + (uint64_t)hdr;
+    const uint32_t v = tid < nt ? tsz[g0 + tid] : 0u;
+    const uint32_t inc = wave_incl_add(v);
+    toff[tid] = base + inc - v;
+    if (tid == 63) toff[kGT] = base + inc;
   }
   __syncthreads();
-  if (hdr && g0 == 0 && tid == 0 && cap > 0) out[0] = (uint8_t)nb_total;
-  for (int k = wv; k < kGT; k += 4) {
-    const size_t t = g0 + k;
-    if (t >= ntiles) break;
-    const uint64_t o0 = toff[k];
-    const uint64_t o1 = min(o0 + tsz[t], cap);
-    if (o1 <= o0) continue;
-    const uint8_t *src = slots + t * (size_t)kSlot;
-    const uintptr_t abs0 = (uintptr_t)(out + o0);
-    const uintptr_t first = abs0 & ~(uintptr_t)15;
-    const uintptr_t absend = (uintptr_t)(out + o1);
-    const int shift = (int)(abs0 - first);
-    const int nchunks = (int)((absend - first + 15) >> 4);
-    for (int ci = lane; ci < nchunks; ci += 64) {
-      const uintptr_t a = first + ((uintptr_t)ci << 4);
-      const int sb = ci * 16 - shift;               // source byte of chunk start
-      if (a >= abs0 && a + 16 <= absend) {
-        const uint4 *q = reinterpret_cast<const uint4 *>(src + (sb & ~15));
-        *reinterpret_cast<uint4 *>(a) = funnel16(q[0], q[1], sb & 15);
-      } else {
-        for (int b = 0; b < 16; ++b) {
-          const uintptr_t ab = a + b;
-          if (ab >= abs0 && ab < absend) *reinterpret_cast<uint8_t *>(ab) = src[sb + b];
-        }
+  if (hdr && g == 0 && tid == 0 && cap > 0) out[0] = (uint8_t)nb_total;
+  const uint64_t G0 = toff[0];
+  const uint64_t G1 = min(toff[nt], cap);
+  if (G1 <= G0) return;
+  const uintptr_t abs0 = (uintptr_t)(out + G0), absend = (uintptr_t)(out + G1);
+  const uintptr_t first = abs0 & ~(uintptr_t)15;
+  const long nchunks = (long)((absend - first + 15) >> 4);
+  int t = 0;                                       // tile cursor (chunks ascend per thread)
+  for (long ci = tid; ci < nchunks; ci += 256) {
+    const uintptr_t a = first + ((uintptr_t)ci << 4);
+    const uint64_t oa = (uint64_t)(a - (uintptr_t)out);   // stream offset of the chunk
+    const uint64_t ob = oa < G0 ? G0 : oa;
+    while (t + 1 < nt && toff[t + 1] <= ob) ++t;
+    const uint8_t *s0 = slots + (g0 + t) * (size_t)kSlot;
+    uint4 v = load16(s0, (long)oa - (long)toff[t]);
+    const uint64_t nx = toff[t + 1];               // next tile's first byte
+    if (t + 1 < nt && nx < oa + 16) {
+      const uint8_t *s1 = slots + (g0 + t + 1) * (size_t)kSlot;
+      v = select16(v, load16(s1, (long)oa - (long)nx), (int)(nx - oa));
+    }
+    if (a >= abs0 && a + 16 <= absend) {
+      *reinterpret_cast<uint4 *>(a) = v;
+    } else {
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const uintptr_t ab = a + b;
+        if (ab >= abs0 && ab < absend)
+          *reinterpret_cast<uint8_t *>(ab) = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
       }
     }
   }
@@ -673,6 +707,7 @@ struct lz4r_ctx {
   uint16_t *bsizes = nullptr;  // encoded bytes of every block of the last call
   uint8_t *slots = nullptr;    // per-tile output slots (kSlot bytes each)
   uint32_t *tsz = nullptr;     // encoded bytes per tile
+  uint32_t *gsum = nullptr;    // encoded bytes per group of kGT tiles
   uint64_t *part = nullptr;    // scan partials, one per kPart tiles
   unsigned max_grid = 0;       // resident workgroups of lz4_tiles on this device
   uint64_t *len = nullptr;     // default device length slot
@@ -686,12 +721,14 @@ namespace {
 
 void free_scratch(lz4r_ctx *c) {
   (void)hipFree(c->bsizes);
-  (void)hipFree(c->slots);
   (void)hipFree(c->tsz);
+  (void)hipFree(c->gsum);
   (void)hipFree(c->part);
+  if (c->slots) (void)hipFree(c->slots - 16);
   c->bsizes = nullptr;
   c->slots = nullptr;
   c->tsz = nullptr;
+  c->gsum = nullptr;
   c->part = nullptr;
   c->cap_blocks = 0;
   c->cap_tiles = 0;
@@ -703,9 +740,16 @@ int ensure_scratch(lz4r_ctx *c, size_t nb) {
   const size_t cap = nb + nb / 8 + 1024;
   const size_t tiles = (cap + kTB - 1) / kTB;
   const size_t parts = (tiles + kPart - 1) / kPart;
+  const size_t groups = (tiles + kGT - 1) / kGT;
+  uint8_t *slots = nullptr;      // 16-B pad in front: gather reads slot - 16
+  if (hipMalloc(&slots, tiles * (size_t)kSlot + 32) != hipSuccess) {
+    free_scratch(c);
+    return LZ4R_ERR_NOMEM;
+  }
+  c->slots = slots + 16;
   if (hipMalloc(&c->bsizes, cap * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&c->slots, tiles * (size_t)kSlot) != hipSuccess ||
       hipMalloc(&c->tsz, tiles * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&c->gsum, groups * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&c->part, parts * sizeof(uint64_t)) != hipSuccess) {
     free_scratch(c);
     return LZ4R_ERR_NOMEM;
@@ -737,12 +781,12 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   if (timed) (void)hipEventRecord(c->ev_b, s);
   const size_t nparts = (ntiles + kPart - 1) / kPart;
   hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)nparts), dim3(256), 0, s, c->tsz, ntiles,
-                     c->part);
+                     c->gsum, c->part);
   hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part, nparts,
                      (uint64_t)hdr, static_cast<uint64_t *>(d_len));
   hipLaunchKernelGGL(lz4_gather, dim3((unsigned)((ntiles + kGT - 1) / kGT)), dim3(256), 0, s,
-                     c->slots, c->tsz, ntiles, c->part, static_cast<uint8_t *>(d_out),
-                     (uint64_t)cap, hdr, (uint64_t)nb);
+                     c->slots, c->tsz, ntiles, c->gsum, c->part,
+                     static_cast<uint8_t *>(d_out), (uint64_t)cap, hdr, (uint64_t)nb);
   if (timed) (void)hipEventRecord(c->ev_c, s);
   c->last_nb = nb;
   return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
