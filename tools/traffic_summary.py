@@ -25,9 +25,10 @@ def per_launch(db, counter, kernel_sub):
 
 def main(d):
     out = {}
-    for kern, sub in (("lz4", "lz4_tiles"), ("jpeg", "jpeg_strip_kernel")):
-        f = per_launch(os.path.join(d, f"{kern}_fetch", "run_results.db"), "FETCH_SIZE", sub)
-        w = per_launch(os.path.join(d, f"{kern}_write", "run_results.db"), "WRITE_SIZE", sub)
+    for kern, run, sub in (("lz4", "lz4", "lz4_tiles"), ("lz4_gather", "lz4", "lz4_gather"),
+                           ("jpeg", "jpeg", "jpeg_strip_kernel")):
+        f = per_launch(os.path.join(d, f"{run}_fetch", "run_results.db"), "FETCH_SIZE", sub)
+        w = per_launch(os.path.join(d, f"{run}_write", "run_results.db"), "WRITE_SIZE", sub)
         if not f or not w:
             continue
         fetch = 2 * 1024 * sum(f) / len(f)
