@@ -66,6 +66,18 @@ int jpegr_time_device(const void *d_rgba, int w, int h, int nimg,
                       void *d_out_i16, int iters, void *stream,
                       float *ms_per_launch);
 
+/* Reconstruction (the decode side of the reference's main, JPEG.c:1131-1425;
+ * the RLE/Huffman round trip there is the identity on the coefficients):
+ * per tile, reverse zigzag + Inverse_quantize (:631-638), fp64 IDCT in the
+ * reference's order with (int)round(x + 128) clamped (:399-448), and
+ * assemble_image's YCbCr 4:2:2 -> RGB (:553-619), RGBA8 out (a = 255).
+ * d_coef is jpegr_encode_device's layout.  Tiles at raster index >=
+ * ceil(w*h/64) are never transformed by the reference (:1131) and keep their
+ * original samples: pass the source image as d_rgba_orig to reproduce that
+ * (NULL decodes them like the others).  Asynchronous on `stream`. */
+int jpegr_reconstruct_device(const void *d_coef, const void *d_rgba_orig, int w, int h,
+                             int nimg, void *d_rgba_out, void *stream);
+
 /* Block-level kernels (jpegr_blocks.hip) behind the reference-named API in
  * lz4jpeg_compat.h, asynchronous on `stream`:
  *   jpegr_planes_device: full-resolution uint8 Y, Cr, Cb planes of an RGBA8

@@ -42,6 +42,8 @@ __constant__ int dLQ[64];
 __constant__ int dCQ[32];
 __constant__ int dZZ8[64];
 __constant__ int dZZ4[32];
+__constant__ int dZZ8inv[64];   // zigzag index -> natural index
+__constant__ int dZZ4inv[32];
 
 __device__ __forceinline__ int clamp_u8(int v) {       // JPEG.c:132-139
   return v < 0 ? 0 : (v > 255 ? 255 : v);
@@ -210,6 +212,170 @@ __global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
   }
 }
 
+// ---- reconstruction: the decode side of the reference's main --------------
+// (JPEG.c:1131-1425 minus the entropy round trip, which is the identity on
+// the coefficients): per tile, reverse zigzag + Inverse_quantize (:631-638),
+// fp64 IDCT in the reference's order (:399-448: for each (x, y) the sum over
+// u outer, v inner of (((au*av)*c)*cos_x)*cos_y, then (int)round(s + 128)
+// clamped), and assemble_image's YCbCr 4:2:2 -> RGB (:553-619).  Tiles at
+// index >= ceil(W*H/64) are never transformed by the reference (:1131) and
+// keep their original samples: taken from `orig` when given.
+// Workgroup = 256 threads on a strip of 32 tiles of one tile row.
+template <bool ORIG>
+__global__ __launch_bounds__(kThreads) void jpeg_recon_kernel(
+    const int16_t *__restrict__ coef, const uint8_t *__restrict__ orig, int w, int h,
+    int tiles_x, int tiles_y, int strips, uint8_t *__restrict__ out) {
+  __shared__ double yac[kTiles * kYStride];     // (au*av)*(c*table), natural order
+  __shared__ double crac[kTiles * kCStride];
+  __shared__ double cbac[kTiles * kCStride];
+  __shared__ uint8_t ys[kTiles * 64], crs[kTiles * 32], cbs[kTiles * 32];
+
+  const int img = blockIdx.y;
+  const int br = blockIdx.x / strips;
+  const int bc0 = (blockIdx.x - br * strips) * kTiles;
+  const int ntiles = min(kTiles, tiles_x - bc0);
+  const size_t img_px = (size_t)w * (size_t)h;
+  const size_t total_blocks = (img_px + 63) / 64;                    // JPEG.c:1131
+  const size_t tile0 = (size_t)br * tiles_x + bc0;                   // raster index
+  const int t = threadIdx.x;
+
+  // ---- phase 1: coefficients -> dequantised, alpha-scaled doubles ---------
+  {
+    const int16_t *src = coef + ((size_t)img * tiles_y * tiles_x + tile0) * 128;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e0 = (k * kThreads + t) * 8;          // 8 int16 per thread per step
+      if (e0 < ntiles * 128) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(src + e0);
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int e = e0 + j, tile = e >> 7, z = e & 127;
+          const double q = (double)(int16_t)(wv[j >> 1] >> (16 * (j & 1)));
+          if (z < 64) {
+            const int nat = dZZ8inv[z];
+            yac[tile * kYStride + nat] = dAA88[nat >> 3][nat & 7] * (q * (double)dLQ[nat]);
+          } else {
+            const int zc = (z - 64) & 31, nat = dZZ4inv[zc];
+            const double a = dAA84[nat >> 2][nat & 3] * (q * (double)dCQ[nat]);
+            if (z < 96) crac[tile * kCStride + nat] = a;
+            else cbac[tile * kCStride + nat] = a;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: IDCT, thread = (tile, x) ----------------------------------
+  {
+    const int tile = t >> 3, x = t & 7;
+    double cx[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) cx[u] = dC8[x][u];
+    {
+      const double *a = yac + tile * kYStride;
+      double s[8];
+#pragma unroll
+      for (int y = 0; y < 8; ++y) s[y] = 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          const double tv = a[u * 8 + v] * cx[u];                         // (..*c)*cos_x
+#pragma unroll
+          for (int y = 0; y < 8; ++y) s[y] = s[y] + tv * jpegr_tables::C8[y][v];
+        }
+      }
+#pragma unroll
+      for (int y = 0; y < 8; ++y) {
+        const int value = (int)round(s[y] + 128.0);                      // JPEG.c:440
+        ys[tile * 64 + x * 8 + y] = (uint8_t)(value < 0 ? 0 : (value > 255 ? 255 : value));
+      }
+    }
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      const double *a = (ch == 0 ? crac : cbac) + tile * kCStride;
+      double s[4];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) s[y] = 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const double tv = a[u * 4 + v] * cx[u];
+#pragma unroll
+          for (int y = 0; y < 4; ++y) s[y] = s[y] + tv * jpegr_tables::C4[y][v];
+        }
+      }
+      uint8_t *dst = (ch == 0 ? crs : cbs) + tile * 32 + x * 4;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int value = (int)round(s[y] + 128.0);
+        dst[y] = (uint8_t)(value < 0 ? 0 : (value > 255 ? 255 : value));
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 3: assemble_image (YCbCr 4:2:2 -> RGB) + coalesced stores ----
+  {
+    const int r = t >> 5, c = t & 31;
+    const int row = br * 8 + r;
+    if (row < h) {
+      const uint8_t *osrc = ORIG ? orig + (size_t)img * img_px * 4 : nullptr;
+      uint8_t *dst = out + (size_t)img * img_px * 4;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int lx0 = half * 128 + c * 4;          // pixel column within the strip
+        uint32_t px[4];
+        bool okp[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int lx = lx0 + k, tile = lx >> 3, col = lx & 7;
+          const int x = bc0 * 8 + lx;
+          okp[k] = tile < ntiles && x < w;
+          px[k] = 0;
+          if (!okp[k]) continue;
+          int Y, Cr, Cb;
+          if (ORIG && tile0 + tile >= total_blocks) {                     // untransformed tile
+            const uint8_t *p = osrc + ((size_t)row * w + x) * 4;
+            const double R0 = p[0], G0 = p[1], B0 = p[2];
+            Y = (int)(uint8_t)(unsigned)(0.299 * R0 + 0.587 * G0 + 0.114 * B0);
+            const int xc = bc0 * 8 + (lx & ~1) + 1;                       // odd column
+            Cr = Cb = 0;
+            if (xc < w) {
+              const uint8_t *q = osrc + ((size_t)row * w + xc) * 4;
+              const double R = q[0], G = q[1], B = q[2];
+              Cr = clamp_u8((int)(0.439 * R - 0.368 * G - 0.071 * B + 128.0));
+              Cb = clamp_u8((int)(-0.148 * R - 0.291 * G + 0.439 * B + 128.0));
+            }
+          } else {
+            Y = ys[tile * 64 + r * 8 + col];
+            Cr = crs[tile * 32 + r * 4 + (col >> 1)];
+            Cb = cbs[tile * 32 + r * 4 + (col >> 1)];
+          }
+          const int R = Y + (int)(1.402 * (double)(Cr - 128));              // JPEG.c:601
+          const int G = Y - (int)(0.344136 * (double)(Cb - 128)) -
+                        (int)(0.714136 * (double)(Cr - 128));
+          const int B = Y + (int)(1.772 * (double)(Cb - 128));
+          px[k] = (uint32_t)clamp_u8(R) | ((uint32_t)clamp_u8(G) << 8) |
+                  ((uint32_t)clamp_u8(B) << 16) | (255u << 24);
+        }
+        const int x0 = bc0 * 8 + lx0;
+        uint8_t *q = dst + ((size_t)row * w + x0) * 4;
+        if (okp[0] && okp[3] && ((((uintptr_t)q) & 15) == 0)) {
+          *reinterpret_cast<uint4 *>(q) = make_uint4(px[0], px[1], px[2], px[3]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (okp[k]) reinterpret_cast<uint32_t *>(q)[k] = px[k];
+        }
+      }
+    }
+  }
+}
+
 bool g_tables_ready[64] = {false};
 
 hipError_t upload_tables() {
@@ -228,6 +394,11 @@ hipError_t upload_tables() {
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dCQ), cq, sizeof(cq))) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ8), z8, sizeof(z8))) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ4), z4, sizeof(z4))) != hipSuccess) return e;
+  int i8[64], i4[32];
+  for (int i = 0; i < 64; ++i) i8[ZZ8_POS[i]] = i;
+  for (int i = 0; i < 32; ++i) i4[ZZ4_POS[i]] = i;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ8inv), i8, sizeof(i8))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ4inv), i4, sizeof(i4))) != hipSuccess) return e;
   if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
   return hipSuccess;
 }
@@ -306,6 +477,29 @@ int jpegr_time_device(const void *d_rgba, int w, int h, int nimg, void *d_out,
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   return rc;
+}
+
+int jpegr_reconstruct_device(const void *d_coef, const void *d_rgba_orig, int w, int h,
+                             int nimg, void *d_rgba_out, void *stream) {
+  if (!d_coef || !d_rgba_out || w <= 0 || h <= 0 || nimg <= 0 || nimg > 65535)
+    return JPEGR_ERR_ARG;
+  if (upload_tables() != hipSuccess) return JPEGR_ERR_HIP;
+  const int tx = (w + 7) / 8, ty = (h + 7) / 8;
+  const int strips = (tx + kTiles - 1) / kTiles;
+  const long long gx = (long long)ty * strips;
+  if (gx > 0x7fffffffLL) return JPEGR_ERR_ARG;
+  dim3 grid((unsigned)gx, (unsigned)nimg);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (d_rgba_orig)
+    hipLaunchKernelGGL(jpeg_recon_kernel<true>, grid, dim3(kThreads), 0, s,
+                       static_cast<const int16_t *>(d_coef),
+                       static_cast<const uint8_t *>(d_rgba_orig), w, h, tx, ty, strips,
+                       static_cast<uint8_t *>(d_rgba_out));
+  else
+    hipLaunchKernelGGL(jpeg_recon_kernel<false>, grid, dim3(kThreads), 0, s,
+                       static_cast<const int16_t *>(d_coef), nullptr, w, h, tx, ty, strips,
+                       static_cast<uint8_t *>(d_rgba_out));
+  return hipGetLastError() == hipSuccess ? JPEGR_OK : JPEGR_ERR_HIP;
 }
 
 const char *jpegr_strerror(int code) {

@@ -6,12 +6,13 @@
  *   reads  ../Assets/Images/rand_8X8.png            (JPEG.c:9, :1102)
  *   writes ../Output-Input/Images/original.png, luminance.png,
  *          rChrominance.png, bChrominance.png       (JPEG.c:1105, :1121-1123)
+ *          ../Output-Input/Images/reconstructed.png (JPEG.c:1408-1428)
  *          ../Output-Input/Images/coefficients.bin  the quantised zigzag
  *          coefficients: int16 LE per 8x8 tile [Y 64][Cr 32][Cb 32], tiles
  *          in raster order (the reference keeps them in memory only)
  *   exit 0; unreadable image: "Error loading image" and exit(1) (JPEG.c:74-78).
- * Colour planes, DCT, quantisation and zigzag run on the GPU (jpegr_*).
- * reconstructed.png (IDCT side, JPEG.c:1408-1423) is not produced yet.
+ * Colour planes, DCT, quantisation, zigzag and the reconstruction (reverse
+ * zigzag, dequantisation, IDCT, YCbCr->RGB) run on the GPU (jpegr_*).
  * Optional argv[1] / argv[2] override the input image / output directory.
  */
 #include <stdint.h>
@@ -53,22 +54,26 @@ int main(int argc, char **argv) {
   }
   const size_t npx = (size_t)w * h;
   const size_t ncoef = jpegr_coef_count(w, h);
-  void *d_rgba = NULL, *d_y = NULL, *d_cr = NULL, *d_cb = NULL, *d_coef = NULL;
+  void *d_rgba = NULL, *d_y = NULL, *d_cr = NULL, *d_cb = NULL, *d_coef = NULL, *d_rec = NULL;
   if (hipMalloc(&d_rgba, npx * 4) != hipSuccess || hipMalloc(&d_y, npx) != hipSuccess ||
+      hipMalloc(&d_rec, npx * 4) != hipSuccess ||
       hipMalloc(&d_cr, npx) != hipSuccess || hipMalloc(&d_cb, npx) != hipSuccess ||
       hipMalloc(&d_coef, ncoef * 2) != hipSuccess)
     fail("device allocation failed");
   if (hipMemcpy(d_rgba, rgba, npx * 4, hipMemcpyHostToDevice) != hipSuccess) fail("copy in");
   if (jpegr_planes_device(d_rgba, w, h, d_y, d_cr, d_cb, NULL) != JPEGR_OK ||
-      jpegr_encode_device(d_rgba, w, h, 1, d_coef, NULL) != JPEGR_OK)
+      jpegr_encode_device(d_rgba, w, h, 1, d_coef, NULL) != JPEGR_OK ||
+      jpegr_reconstruct_device(d_coef, d_rgba, w, h, 1, d_rec, NULL) != JPEGR_OK)
     fail("kernel launch");
   uint8_t *y = malloc(npx), *cr = malloc(npx), *cb = malloc(npx), *vis = malloc(npx * 4);
+  uint8_t *rec = malloc(npx * 4);
   int16_t *coef = malloc(ncoef * 2);
-  if (!y || !cr || !cb || !vis || !coef) fail("out of memory");
+  if (!y || !cr || !cb || !vis || !coef || !rec) fail("out of memory");
   if (hipMemcpy(y, d_y, npx, hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(cr, d_cr, npx, hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(cb, d_cb, npx, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(coef, d_coef, ncoef * 2, hipMemcpyDeviceToHost) != hipSuccess)
+      hipMemcpy(coef, d_coef, ncoef * 2, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(rec, d_rec, npx * 4, hipMemcpyDeviceToHost) != hipSuccess)
     fail("copy out");
 
   write_png(out_dir, "original.png", w, h, rgba);                    /* JPEG.c:1105 */
@@ -91,6 +96,7 @@ int main(int argc, char **argv) {
     vis[4 * i + 3] = 255;
   }
   write_png(out_dir, "bChrominance.png", w, h, vis);
+  write_png(out_dir, "reconstructed.png", w, h, rec);                 /* JPEG.c:1428 */
 
   char path[4096];
   snprintf(path, sizeof path, "%scoefficients.bin", out_dir);
@@ -98,7 +104,7 @@ int main(int argc, char **argv) {
   if (!f || fwrite(coef, 2, ncoef, f) != ncoef) fail("cannot write coefficients.bin");
   fclose(f);
   (void)hipFree(d_rgba); (void)hipFree(d_y); (void)hipFree(d_cr); (void)hipFree(d_cb);
-  (void)hipFree(d_coef);
-  free(rgba); free(y); free(cr); free(cb); free(vis); free(coef);
+  (void)hipFree(d_coef); (void)hipFree(d_rec);
+  free(rgba); free(y); free(cr); free(cb); free(vis); free(coef); free(rec);
   return 0;
 }

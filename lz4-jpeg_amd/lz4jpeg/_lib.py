@@ -37,6 +37,7 @@ SIGNATURES = [
     ("jpegr_dct_raw_device", _i, [_vp, _i, _i, _i, _vp, _vp]),
     ("jpegr_encode", _i, [_vp, _i, _i, _vp]),
     ("jpegr_time_device", _i, [_vp, _i, _i, _i, _vp, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
+    ("jpegr_reconstruct_device", _i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     ("jpegr_planes_device", _i, [_vp, _i, _i, _vp, _vp, _vp, _vp]),
     ("jpegr_dct_blocks_device", _i, [_vp, _i, _i, _i, _vp, _vp]),
     ("jpegr_quantize_device", _i, [_vp, _vp, _i, _c_size, _vp]),

@@ -75,3 +75,19 @@ def encode(rgba):
     if rc != 0:
         raise JpegError(rc, "jpegr_encode")
     return out.reshape(-1, 128)
+
+
+def reconstruct_device(d_coef, w, h, nimg=1, d_orig=None, stream=None):
+    """Reconstructed RGBA8 (uint8 tensor nimg*h*w*4) from encode_device's
+    coefficients: reverse zigzag, dequantisation, fp64 IDCT, YCbCr->RGB
+    (JPEG.c:1408-1425).  d_orig reproduces the reference's untransformed
+    trailing tiles (see jpegr.h)."""
+    import torch
+    out = torch.empty(nimg * w * h * 4, dtype=torch.uint8, device=d_coef.device)
+    rc = _lib.lib().jpegr_reconstruct_device(
+        ctypes.c_void_p(d_coef.data_ptr()),
+        ctypes.c_void_p(d_orig.data_ptr() if d_orig is not None else 0), w, h, nimg,
+        ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+    if rc != 0:
+        raise JpegError(rc, "jpegr_reconstruct_device")
+    return out

@@ -272,3 +272,98 @@ void jo_rand_image(unsigned seed, int w, int h, uint8_t *rgba)
         rgba[4 * i + 3] = 255;
     }
 }
+
+/* ---- reconstruction (the decode side of the reference's main) ----------- */
+
+/* inverse_discrete_cosine_transform, JPEG.c:399-448: for x < H, y < W,
+ * sum over u (outer) and v (inner) of ((((au*av)*c)*cos_x)*cos_y), then
+ * (int)round(sum + 128) clamped to [0, 255]. */
+void jo_idct(const double *coef, size_t width, size_t height, uint8_t *values)
+{
+    double cx[8][8], cy[8][8];
+    for (size_t x = 0; x < height; x++)
+        for (size_t u = 0; u < height; u++)
+            cx[x][u] = cos((JO_PI * (2 * x + 1) * u) / (2.0 * height)); /* :425 */
+    for (size_t y = 0; y < width; y++)
+        for (size_t v = 0; v < width; v++)
+            cy[y][v] = cos((JO_PI * (2 * y + 1) * v) / (2.0 * width));  /* :426 */
+    for (size_t x = 0; x < height; x++)
+        for (size_t y = 0; y < width; y++) {
+            double sum = 0.0;
+            for (size_t u = 0; u < height; u++)
+                for (size_t v = 0; v < width; v++) {
+                    double au = (u == 0) ? sqrt(1.0 / height) : sqrt(2.0 / height);
+                    double av = (v == 0) ? sqrt(1.0 / width) : sqrt(2.0 / width);
+                    sum += au * av * coef[u * width + v] * cx[x][u] * cy[y][v];  /* :428 */
+                }
+            int value = (int)round(sum + 128.0);                        /* :440 */
+            values[x * width + y] = value < 0 ? 0 : (value > 255 ? 255 : (uint8_t)value);
+        }
+}
+
+/* zigzag positions of a width x height block: pos[k] = natural index of
+ * zigzag element k (jo_zigzag's order; reverse_zigzag_pattern, JPEG.c:729-764,
+ * visits the same cells in the same order) */
+static void jo_zigzag_pos(size_t width, size_t height, int *pos)
+{
+    double nat[64], zz[64];
+    for (size_t i = 0; i < width * height; i++) nat[i] = (double)i;
+    jo_zigzag(width, height, nat, zz);
+    for (size_t k = 0; k < width * height; k++) pos[k] = (int)zz[k];
+}
+
+/* One tile's reconstructed samples from its 128 zigzag int16 coefficients:
+ * reverse zigzag, Inverse_quantize (JPEG.c:631-638), IDCT. */
+void jo_decode_tile(const int16_t *coef, uint8_t ylum[64], uint8_t cr[32], uint8_t cb[32])
+{
+    int p8[64], p4[32];
+    jo_zigzag_pos(8, 8, p8);
+    jo_zigzag_pos(4, 8, p4);
+    double c[64];
+    for (int k = 0; k < 64; k++) c[p8[k]] = (double)coef[k];
+    for (int i = 0; i < 64; i++) c[i] *= JO_LUMA_Q[i];
+    jo_idct(c, 8, 8, ylum);
+    for (int k = 0; k < 32; k++) c[p4[k]] = (double)coef[64 + k];
+    for (int i = 0; i < 32; i++) c[i] *= JO_CHROMA_Q[i];
+    jo_idct(c, 4, 8, cr);
+    for (int k = 0; k < 32; k++) c[p4[k]] = (double)coef[96 + k];
+    for (int i = 0; i < 32; i++) c[i] *= JO_CHROMA_Q[i];
+    jo_idct(c, 4, 8, cb);
+}
+
+/* reconstructed.png pixels (JPEG.c:1131-1425): tiles below
+ * ceil(W*H/64) are decoded; the rest keep their original tile samples (the
+ * reference never transforms them, :1131, but assemble_image walks every
+ * tile); assemble_image (JPEG.c:553-619) converts YCbCr 4:2:2 to RGB. */
+void jo_reconstruct_image(const uint8_t *rgba, int w, int h, uint8_t *out)
+{
+    const int tx = jo_tiles_x(w), ty = jo_tiles_y(h);
+    const size_t total_blocks = ((size_t)w * h + 63) / 64;
+    for (int br = 0; br < ty; br++)
+        for (int bc = 0; bc < tx; bc++) {
+            const size_t i = (size_t)br * tx + bc;
+            uint8_t yl[64], cr[32], cb[32];
+            if (i < total_blocks) {
+                int16_t q[128];
+                jo_encode_tile(rgba, w, h, br, bc, q);
+                jo_decode_tile(q, yl, cr, cb);
+            } else {
+                jo_tile_inputs(rgba, w, h, br, bc, yl, cr, cb);
+            }
+            for (int r = 0; r < 8; r++)
+                for (int c = 0; c < 8; c++) {
+                    const int row = 8 * br + r, col = 8 * bc + c;
+                    if (row >= h || col >= w) continue;
+                    const int Y = yl[r * 8 + c];
+                    const int Cb = cb[r * 4 + c / 2], Cr = cr[r * 4 + c / 2];
+                    int R = Y + (int)(1.402 * (Cr - 128));                 /* :601 */
+                    int G = Y - (int)(0.344136 * (Cb - 128)) - (int)(0.714136 * (Cr - 128));
+                    int B = Y + (int)(1.772 * (Cb - 128));
+                    uint8_t *o = out + ((size_t)row * w + col) * 4;
+                    o[0] = jo_clamp(R);
+                    o[1] = jo_clamp(G);
+                    o[2] = jo_clamp(B);
+                    o[3] = 255;
+                }
+        }
+}

@@ -115,3 +115,119 @@ int ref_jpeg_dct_raw(const unsigned char *rgba, int w, int h, double *out)
     free_pixels(img.pixels, h);
     return 0;
 }
+
+/* The reference's whole per-block pipeline after the DCT, as its main()
+ * runs it (JPEG.c:1131-1423): Quantize, zigzag, RLE, the per-block Huffman
+ * encode -> decode round trip, inverse RLE, reverse zigzag,
+ * Inverse_quantize, IDCT for the first ceil(W*H/64) blocks, then
+ * assemble_image over every tile.  out_rgba receives the pixels main()
+ * writes to reconstructed.png. */
+int ref_jpeg_reconstruct(const unsigned char *rgba, int w, int h, unsigned char *out_rgba)
+{
+    ImageData img;
+    img.width = w;
+    img.height = h;
+    img.pixel_count = (size_t)w * h;
+    img.pixels = malloc(h * sizeof(Pixel *));
+    for (int y = 0; y < h; y++) {
+        img.pixels[y] = malloc(w * sizeof(Pixel));
+        for (int x = 0; x < w; x++) {
+            const unsigned char *p = rgba + ((size_t)y * w + x) * 4;
+            img.pixels[y][x].r = p[0];
+            img.pixels[y][x].g = p[1];
+            img.pixels[y][x].b = p[2];
+            img.pixels[y][x].a = p[3];
+        }
+    }
+    uint8_t **lum, **cr, **cb;
+    build_luminance_matrix(img, &lum);
+    build_rChrominance_matrix(img, &cr);
+    build_bChrominance_matrix(img, &cb);
+    chroma_subsample(&cb, img);
+    chroma_subsample(&cr, img);
+    size_t total_blocks = (size_t)ceil((double)img.pixel_count / 64);      /* :1131 */
+    PixelGroup *blocks = divide_image(lum, cr, cb, img, 8);
+    for (size_t i = 0; i < total_blocks; i++) {                              /* :1136-1149 */
+        discrete_cosine_transform(blocks[i].lum_values, 8, 8, &blocks[i].lum_coefficients);
+        discrete_cosine_transform(blocks[i].r_values, 4, 8, &blocks[i].r_coefficients);
+        discrete_cosine_transform(blocks[i].b_values, 4, 8, &blocks[i].b_coefficients);
+        Quantize(&blocks[i].lum_coefficients, LUMINANCE_QUANTIZATION_TABLE, 64);
+        Quantize(&blocks[i].b_coefficients, CHROMINANCE_QUANTIZATION_TABLE, 32);
+        Quantize(&blocks[i].r_coefficients, CHROMINANCE_QUANTIZATION_TABLE, 32);
+    }
+    for (size_t i = 0; i < total_blocks; i++) {                              /* :1159-1405 */
+        double tl[64], tr[32], tb[32];
+        zigzag_pattern(8, 8, blocks[i].lum_coefficients, tl);
+        zigzag_pattern(4, 8, blocks[i].r_coefficients, tr);
+        zigzag_pattern(4, 8, blocks[i].b_coefficients, tb);
+        for (size_t j = 0; j < 64; j++) blocks[i].lum_coefficients[j] = tl[j];
+        for (size_t j = 0; j < 32; j++) {
+            blocks[i].r_coefficients[j] = tr[j];
+            blocks[i].b_coefficients[j] = tb[j];
+        }
+        size_t ll, lr, lb;
+        RLE(tl, 64, &blocks[i].RLE_encoded_lum, &ll);
+        RLE(tr, 32, &blocks[i].RLE_encoded_r, &lr);
+        RLE(tb, 32, &blocks[i].RLE_encoded_b, &lb);
+        int *enc[3] = {blocks[i].RLE_encoded_lum, blocks[i].RLE_encoded_r, blocks[i].RLE_encoded_b};
+        size_t el[3] = {ll, lr, lb};
+        for (int c = 0; c < 3; c++) {
+            size_t ncode;
+            Node *root;
+            HuffmanCode *codes = encode_huffman(enc[c], el[c], &ncode, &root);
+            char seq[2048];
+            generate_encoded_sequence(enc[c], el[c], codes, ncode, seq);
+            size_t dl;
+            double *dec = decode_huffman(root, seq, &dl);
+            for (size_t j = 0; j < dl; j++) enc[c][j] = (int)dec[j];
+            free(codes);
+            free(dec);
+        }
+        inverse_RLE(blocks[i].RLE_encoded_lum, blocks[i].lum_coefficients, 64, ll);
+        inverse_RLE(blocks[i].RLE_encoded_r, blocks[i].r_coefficients, 32, lr);
+        inverse_RLE(blocks[i].RLE_encoded_b, blocks[i].b_coefficients, 32, lb);
+        double rl[64], rr[32], rb[32];
+        reverse_zigzag_pattern(8, 8, blocks[i].lum_coefficients, rl);
+        reverse_zigzag_pattern(4, 8, blocks[i].r_coefficients, rr);
+        reverse_zigzag_pattern(4, 8, blocks[i].b_coefficients, rb);
+        for (size_t j = 0; j < 64; j++) blocks[i].lum_coefficients[j] = rl[j];
+        for (size_t j = 0; j < 32; j++) {
+            blocks[i].r_coefficients[j] = rr[j];
+            blocks[i].b_coefficients[j] = rb[j];
+        }
+    }
+    for (size_t i = 0; i < total_blocks; i++) {                              /* :1408-1413 */
+        Inverse_quantize(&(blocks[i].lum_coefficients), LUMINANCE_QUANTIZATION_TABLE, 64);
+        Inverse_quantize(&(blocks[i].b_coefficients), CHROMINANCE_QUANTIZATION_TABLE, 32);
+        Inverse_quantize(&(blocks[i].r_coefficients), CHROMINANCE_QUANTIZATION_TABLE, 32);
+    }
+    for (size_t i = 0; i < total_blocks; i++) {                              /* :1416-1421 */
+        inverse_discrete_cosine_transform(blocks[i].lum_values, 8, 8, blocks[i].lum_coefficients);
+        inverse_discrete_cosine_transform(blocks[i].b_values, 4, 8, blocks[i].b_coefficients);
+        inverse_discrete_cosine_transform(blocks[i].r_values, 4, 8, blocks[i].r_coefficients);
+    }
+    ImageData rec = {0};
+    assemble_image(&rec, img, blocks);                                       /* :1425 */
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            unsigned char *o = out_rgba + ((size_t)y * w + x) * 4;
+            o[0] = rec.pixels[y][x].r;
+            o[1] = rec.pixels[y][x].g;
+            o[2] = rec.pixels[y][x].b;
+            o[3] = rec.pixels[y][x].a;
+        }
+    for (size_t i = 0; i < total_blocks; i++) {
+        free(blocks[i].lum_coefficients);
+        free(blocks[i].r_coefficients);
+        free(blocks[i].b_coefficients);
+        free(blocks[i].RLE_encoded_lum);
+        free(blocks[i].RLE_encoded_r);
+        free(blocks[i].RLE_encoded_b);
+    }
+    free(blocks);
+    for (int y = 0; y < h; y++) { free(lum[y]); free(cr[y]); free(cb[y]); }
+    free(lum); free(cr); free(cb);
+    free_pixels(img.pixels, h);
+    free_pixels(rec.pixels, h);
+    return 0;
+}

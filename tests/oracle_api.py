@@ -98,3 +98,26 @@ def ref_jpeg():
     L.ref_jpeg_encode_image.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp]
     L.ref_jpeg_dct_raw.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp]
     return L
+
+
+def reconstruct(oracle, rgba):
+    """Oracle restatement of reconstructed.png's pixels."""
+    h, w = rgba.shape[:2]
+    a = np.ascontiguousarray(rgba, dtype=np.uint8)
+    out = np.empty((h, w, 4), np.uint8)
+    oracle.L.jo_reconstruct_image.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp]
+    oracle.L.jo_reconstruct_image(a.ctypes.data_as(_vp), w, h, out.ctypes.data_as(_vp))
+    return out
+
+
+def ref_reconstruct(rgba):
+    """The reference's own pipeline (JPEG.c main, via oracle/_ref), or None."""
+    L = ref_jpeg()
+    if L is None:
+        return None
+    h, w = rgba.shape[:2]
+    a = np.ascontiguousarray(rgba, dtype=np.uint8)
+    out = np.empty((h, w, 4), np.uint8)
+    L.ref_jpeg_reconstruct.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp]
+    L.ref_jpeg_reconstruct(a.ctypes.data_as(_vp), w, h, out.ctypes.data_as(_vp))
+    return out

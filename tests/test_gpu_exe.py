@@ -91,6 +91,9 @@ def test_jpeg_seq_file_contract(tmp_path, oracle, w, h):
     assert np.array_equal(lum[..., 0], y) and np.array_equal(lum[..., 2], y)
     for name in ("rChrominance.png", "bChrominance.png"):
         assert (tmp_path / "Output-Input/Images" / name).exists()
+    import oracle_api
+    rec = pngdec.read(str(tmp_path / "Output-Input/Images/reconstructed.png"))
+    assert np.array_equal(rec, oracle_api.reconstruct(oracle, img))
 
 
 def test_jpeg_seq_missing_image_exits_1(tmp_path):

@@ -83,3 +83,20 @@ def test_jpeg_oracle_vs_reference_build(oracle):
         rraw = np.empty_like(raw)
         ref.ref_jpeg_dct_raw(img.ctypes.data, w, h, rraw.ctypes.data)
         assert raw.tobytes() == rraw.tobytes(), (w, h)
+
+
+@pytest.mark.parametrize("w,h,seed", [(8, 8, 1), (64, 48, 2), (38, 21, 3), (2, 1, 4), (4, 4, 5),
+                                      (120, 63, 6), (256, 256, 7), (1200, 630, 8)])
+def test_reconstruction_oracle_matches_reference(oracle, w, h, seed):
+    """jo_reconstruct_image == the reference's whole pipeline (JPEG.c main:
+    DCT, Quantize, zigzag, RLE, Huffman round trip, inverse RLE, reverse
+    zigzag, Inverse_quantize, IDCT, assemble_image), compiled from its
+    sources.  Sizes that are not tile multiples exercise the ceil(W*H/64)
+    block-count quirk (38x21: 15 tiles, 13 transformed).  Widths are even:
+    for odd widths divide_image reads Cs[row][W/2], one past the
+    malloc(W/2) row (JPEG.c:541-544, :316) -- undefined; we define it as 0."""
+    ref = oracle_api.ref_reconstruct(oracle.rand_image(w, h, seed=seed))
+    if ref is None:
+        pytest.skip("reference not built")
+    got = oracle_api.reconstruct(oracle, oracle.rand_image(w, h, seed=seed))
+    assert np.array_equal(got, ref)
