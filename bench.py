@@ -150,6 +150,40 @@ def main():
         barrier()
         gather_ms = max_over_ranks(time.perf_counter() - g0) * 1e3
 
+    # decoder: this rank's framed stream -> bytes, in HBM
+    _, flen = comp.compress_device(d_in, n, d_out)
+    nb_local = ldist.nblocks(n)
+    d_boff = torch.from_numpy(comp.block_offsets(nb_local).astype(np.int64)).to(dev)
+    d_dec = torch.empty(n + 300, dtype=torch.uint8, device=dev)
+    _, got = lz4.decompress_device(d_out, flen, d_boff, nb_local, n + 300, d_out=d_dec)
+    dec_ok = got == n and bool(torch.equal(d_dec[:n], d_in))
+    torch.cuda.synchronize()
+    barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        lz4.decompress_device(d_out, flen, d_boff, nb_local, n + 300, d_out=d_dec,
+                              check=False)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    ddt = max_over_ranks(time.perf_counter() - t0)
+    dec_kern_ms = e0.elapsed_time(e1) / args.steps
+    lz4_dec = {
+        "metric": "LZ4 block-parallel decode GB/s (decoded bytes, stream resident in HBM)",
+        "value": round(n_total / (ddt / args.steps) / 1e9, 3), "unit": "GB/s",
+        "kernel": "lz4_decode_blocks", "avg_launch_ms": round(dec_kern_ms, 4),
+        "roundtrip_ok": dec_ok,
+        "roofline": {
+            "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+            "achieved": round((n + flen) / (dec_kern_ms / 1e3) / 1e9, 2),
+            "frac": round((n + flen) / (dec_kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "algorithmic bytes = compressed bytes read + decoded bytes written"},
+    }
+    del d_dec
+    log(f"lz4 decode: {dec_kern_ms:.3f} ms/launch, {lz4_dec['value']} GB/s, ok={dec_ok}")
+
     roof_lz4 = {
         "bound": "hbm", "kernel": "lz4_tiles",
         "achieved": round(n / (avg_match_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
@@ -220,6 +254,32 @@ def main():
         }
         log(f"jpeg: {jres['ms_per_step']} ms/step, {gpix:.2f} Gpix/s aggregate, kernel {kern_ms:.4f} ms")
 
+        # reconstruction: coefficients -> reconstructed RGBA
+        d_rec_out = jpeg.reconstruct_device(d_coef, W, H, B, d_orig=d_img)
+        torch.cuda.synchronize()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record(stream)
+        for _ in range(jsteps):
+            jpeg.reconstruct_device(d_coef, W, H, B, d_orig=d_img)
+        r1.record(stream)
+        torch.cuda.synchronize()
+        rec_ms = r0.elapsed_time(r1) / jsteps
+        del d_rec_out
+        jres["reconstruct"] = {
+            "metric": "JPEG reconstruction (dequant + fp64 IDCT + YCbCr->RGB) Gpixel/s",
+            "value": round(px_rank / (rec_ms / 1e3) / 1e9, 3), "unit": "Gpixel/s",
+            "kernel": "jpeg_recon_kernel", "avg_launch_ms": round(rec_ms, 4),
+            "roofline": {
+                "bound": "valu_fp64", "unit": "Tops/s", "peak": FP64_VALU_PEAK_TOPS,
+                "achieved": round(tiles * 13568 / (rec_ms / 1e3) / 1e12, 2),
+                "frac": round(tiles * 13568 / (rec_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
+                "hbm_gbs": round(8 * px_rank / (rec_ms / 1e3) / 1e9, 2),
+                "note": "13568 non-fused fp64 mul/add per tile (dequant x alpha 2x128, luma 8x(64 + 1024), "
+                        "chroma 2x8x(32 + 256)); 8 B/px algorithmic HBM "
+                        "(4 B int16 read + 4 B RGBA written)"},
+        }
+        log(f"jpeg reconstruct: {rec_ms:.4f} ms, {jres['reconstruct']['value']} Gpix/s")
+
     # --------------------------------------------------------- CPU baselines
     cpu_lz4 = cpu_jpeg = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -239,6 +299,7 @@ def main():
             "roofline": roof_lz4,
             "cpu_baseline": cpu_lz4,
             "lz4_gather_ms": None if gather_ms is None else round(gather_ms, 3),
+            "lz4_decode": lz4_dec,
             "jpeg": jres,
         }
         if jres is not None:

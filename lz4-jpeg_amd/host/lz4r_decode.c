@@ -10,6 +10,8 @@
  *   - blocks are parsed until the input ends; the frame byte is checked
  *     against the block count modulo 256;
  *   - L is recovered from the sequence's u16 size field, which is exact;
+ *   - the block header's u16 size field must equal 3 + the sum of its
+ *     sequences' size fields (LZ4.c:617), which also prunes wrong readings;
  *   - the format has one genuine ambiguity: a match of length 257..259 is
  *     stored as M = 1..3 (uint8 truncation, LZ4.c:317) and its token
  *     ((L<<4) | (M-4)&0xFF) & 0xFF reads 0xFD..0xFF whatever L was -- the
@@ -31,6 +33,8 @@ typedef struct {
   size_t ip_end;         /* input position after the block (on success) */
   size_t out_len;        /* decoded length of the block (on success) */
   unsigned nseq;
+  size_t want;           /* the block header's size field minus 3 = sum of the
+                            sequences' size fields (LZ4.c:617) */
 } dec_block;
 
 static unsigned litext_len(size_t L) {
@@ -47,9 +51,10 @@ static int litext_ok(const uint8_t *in, size_t in_len, size_t ip, size_t L) {
 
 /* Decode sequences s.. of the block from input position ip with `pos` bytes
  * of the block already produced.  Returns 1 on a consistent full parse. */
-static int dec_seq(dec_block *d, unsigned s, size_t ip, size_t pos) {
+static int dec_seq(dec_block *d, unsigned s, size_t ip, size_t pos, size_t ssum) {
   const uint8_t *in = d->in;
   if (s == d->nseq) {
+    if (ssum != d->want) return 0;
     if ((pos == LZ4R_BLOCK && ip < d->in_len) || (ip == d->in_len && pos >= 1 && pos <= LZ4R_BLOCK)) {
       d->ip_end = ip;
       d->out_len = pos;
@@ -61,6 +66,7 @@ static int dec_seq(dec_block *d, unsigned s, size_t ip, size_t pos) {
   const unsigned tok = in[ip];
   const size_t S = (size_t)in[ip + 1] | ((size_t)in[ip + 2] << 8);
   const size_t ip0 = ip + 3;
+  if (ssum + S > d->want) return 0;
   const int last = (s + 1 == d->nseq);
 
   /* reading A: token nibbles as written for M == 0 or M >= 4 */
@@ -98,7 +104,7 @@ static int dec_seq(dec_block *d, unsigned s, size_t ip, size_t pos) {
         memcpy(d->blk + pos, in + ip1, L);
         size_t p = pos + L;
         for (size_t k = 0; k < M; ++k, ++p) d->blk[p] = d->blk[p - dist];
-        if (dec_seq(d, s + 1, ip2, p)) return 1;
+        if (dec_seq(d, s + 1, ip2, p, ssum + S)) return 1;
       }
     }
   }
@@ -119,7 +125,7 @@ static int dec_seq(dec_block *d, unsigned s, size_t ip, size_t pos) {
       memcpy(d->blk + pos, in + ip1, L);
       size_t p = pos + L;
       for (size_t k = 0; k < M; ++k, ++p) d->blk[p] = d->blk[p - dist];
-      if (dec_seq(d, s + 1, ip1 + L + 2, p)) return 1;
+      if (dec_seq(d, s + 1, ip1 + L + 2, p, ssum + S)) return 1;
     }
   }
   return 0;
@@ -133,8 +139,10 @@ int lz4r_decompress(const uint8_t *in, size_t in_len, uint8_t *out, size_t cap,
   size_t ip = 1, op = 0, nb = 0;
   while (ip < in_len) {
     if (ip + 3 > in_len) return LZ4R_ERR_CORRUPT;
-    dec_block d = {in, in_len, blk, 0, 0, in[ip]};
-    if (!dec_seq(&d, 0, ip + 3, 0)) return LZ4R_ERR_CORRUPT;
+    const size_t bsize = (size_t)in[ip + 1] | ((size_t)in[ip + 2] << 8);
+    if (bsize < 3) return LZ4R_ERR_CORRUPT;
+    dec_block d = {in, in_len, blk, 0, 0, in[ip], bsize - 3};
+    if (!dec_seq(&d, 0, ip + 3, 0, 0)) return LZ4R_ERR_CORRUPT;
     if (op + d.out_len > cap) {
       *out_len = op + d.out_len;
       return LZ4R_ERR_CAPACITY;

@@ -28,6 +28,7 @@ SIGNATURES = [
     ("lz4r_copy_block_offsets", _i, [_vp, _vp, _c_size, _vp]),
     ("lz4r_compress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
     ("lz4r_decompress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
+    ("lz4r_decompress_device", _i, [_vp, _c_size, _vp, _c_size, _vp, _c_size, _vp, _vp]),
     ("lz4r_set_timing", _i, [_vp, _i]),
     ("lz4r_last_timing", _i, [_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ("lz4r_strerror", ctypes.c_char_p, [_i]),
@@ -102,5 +103,6 @@ LZ4R_ERR_TOO_SMALL = -2
 LZ4R_ERR_CAPACITY = -3
 LZ4R_ERR_HIP = -4
 LZ4R_ERR_NOMEM = -5
+LZ4R_ERR_CORRUPT = -6
 LZ4R_BLOCK = 300
 LZ4R_BLOCK_BOUND = 1152

@@ -15,7 +15,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import Lz4Error, LZ4R_BLOCK, LZ4R_BLOCK_BOUND
+from ._lib import Lz4Error, LZ4R_BLOCK, LZ4R_BLOCK_BOUND  # noqa: F401
 
 BLOCK = LZ4R_BLOCK
 
@@ -158,3 +158,29 @@ def decompress(stream, cap=None):
     if rc != 0:
         _raise(rc, "lz4r_decompress")
     return out[:got.value].tobytes()
+
+
+def decompress_device(d_stream, length, d_offsets, nb, out_cap, d_out=None, stream=None,
+                      check=True):
+    """Block-parallel GPU decode (lz4r_decompress_device).  d_stream: uint8
+    tensor holding the framed stream (first `length` bytes); d_offsets: int64
+    tensor of nb per-block offsets (Compressor.block_offsets).  Returns
+    (d_out, decoded_length); raises Lz4Error(-6) naming the first malformed
+    block.  check=False skips the result read-back (no host sync) and
+    returns (d_out, None)."""
+    import torch
+    if d_out is None:
+        d_out = torch.empty(max(out_cap, 1), dtype=torch.uint8, device=d_stream.device)
+    res = torch.empty(2, dtype=torch.int64, device=d_stream.device)
+    rc = _lib.lib().lz4r_decompress_device(
+        ctypes.c_void_p(d_stream.data_ptr()), length, ctypes.c_void_p(d_offsets.data_ptr()), nb,
+        ctypes.c_void_p(d_out.data_ptr()), out_cap, ctypes.c_void_p(res.data_ptr()),
+        _stream_handle(stream))
+    if rc != 0:
+        _raise(rc, "lz4r_decompress_device")
+    if not check:
+        return d_out, None
+    n, bad = (int(x) for x in res.cpu().tolist())
+    if bad != -1:
+        raise Lz4Error(_lib.LZ4R_ERR_CORRUPT, f"lz4r_decompress_device: block {bad - 1}")
+    return d_out, n

@@ -67,3 +67,13 @@ def test_corrupt_streams_rejected(oracle):
         lz4.decompress(bytes(bad))
     with pytest.raises(Lz4Error):
         lz4.decompress(b"")
+
+
+def test_block_size_field_checked(oracle):
+    """The block header's u16 size (3 + sum of sequence size fields,
+    LZ4.c:617) is validated."""
+    data = golden_inputs.lz4_input("text_10000")
+    comp = bytearray(oracle.lz4_compress(data))
+    comp[2] ^= 0x40                                     # block 0's size field
+    with pytest.raises(Lz4Error):
+        lz4.decompress(bytes(comp))
