@@ -109,14 +109,15 @@ int lz4r_copy_block_offsets(const lz4r_ctx *ctx, void *dst, size_t count,
 int lz4r_decompress(const uint8_t *in, size_t in_len, uint8_t *out, size_t cap,
                     size_t *out_len);
 
-/* Block-parallel GPU decoder (csrc/lz4r_decode.hip), asynchronous on
+/* Block-parallel GPU decoder (csrc/lz4r_gpudec.hip), asynchronous on
  * `stream`.  d_in: the framed stream (in_len bytes, device); d_block_offsets:
  * nb uint64 offsets of each block's first byte relative to the first block
  * byte, as lz4r_copy_block_offsets returns them for the compressing call
  * (the format cannot be split without them).  Block b decodes to
  * d_out[300 b ...]; nothing at or past out_cap is written.  d_result: two
- * uint64 on the device: [0] = decoded length, [1] = ~0 if every block was
- * consistent, else 1 + the index of the first malformed block. */
+ * uint64 on the device: [0] = decoded length (if it exceeds out_cap, only
+ * out_cap bytes were written), [1] = ~0 if every block was consistent, else
+ * 1 + the index of the first malformed block. */
 int lz4r_decompress_device(const void *d_in, size_t in_len, const void *d_block_offsets,
                            size_t nb, void *d_out, size_t out_cap, void *d_result,
                            void *stream);

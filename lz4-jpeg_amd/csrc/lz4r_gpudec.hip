@@ -9,24 +9,33 @@
 // split in parallel (the u16 size field over-counts the truncated-length
 // sequences, LZ4.c:569-575).
 //
-// Mapping: one LANE per block, 64 consecutive blocks per wave.  Parsing a
-// block is a serial walk over its sequence headers; running 64 of them side
-// by side makes each wave instruction do 64 blocks' work (a wave-per-block
-// walk issues the same instructions for one block).  Each lane
-//   parse  reads its block straight from global memory (aligned dword loads,
-//          L1/L2 absorb the re-reads; the wave's 64 blocks are one
-//          contiguous ~20 KB range).  L comes from the exact u16 size field;
-//          the one ambiguous token family (0xFD..0xFF: L >= 15 with
-//          M = 17 / 18 / >= 19, or a truncated match M = 1..3 whatever L,
-//          LZ4.c:317 + :540-544) is resolved by a per-lane LDS stack of
-//          choice points: the plain reading is taken first and undone if the
-//          block does not then end exactly at its last byte with 300 decoded
-//          bytes (or 1..300 for the last block) and size fields summing to
-//          the block header's (LZ4.c:617).  A plain reading of such a token
-//          decodes >= 32 bytes, so at most 9 choice points are ever pending.
-//   emit   writes literals and (periodic) match copies into its 300-byte
-//          LDS slot as it parses; a backtrack simply rewrites the tail.
-// The wave then stores its 64 x 300 = 19200 contiguous bytes as 16-B stores.
+// Mapping: one LANE per block, 64 consecutive blocks per wave (a wave per
+// block would issue every serial parsing step as a full wave instruction).
+// The walk is latency- and issue-bound, so the kernel keeps LDS small for
+// occupancy (22 KB per wave: the 64 output slots + the choice stack) and
+// keeps instruction counts low:
+//   - the lane reads its encoded bytes with single unaligned 8/16-byte
+//     global loads (L1/L2 absorb the re-reads of the wave's ~20 KB range);
+//   - a sequence header is decoded branch-free for the plain reading; the
+//     rare truncated readings (below) take a separate path;
+//   - literals move in 16-byte chunks; a match of distance D is copied in
+//     chunks of min(16, d) bytes at a distance d that grows from D (the
+//     match is D-periodic, so any multiple of D up to the bytes already
+//     written + D is a valid distance), with D < 8 seeded by replicating
+//     its period over 8 bytes;
+//   - stores into the LDS slot are exact-size (b64/b32/b16/b8 pieces, the
+//     hardware runs in unaligned mode), so no lane touches a neighbour's slot;
+//   - the wave's 64 x 300 = 19200 contiguous bytes leave as 16-B stores.
+// L comes from the exact u16 size field; the one ambiguous token family
+// (0xFD..0xFF: L >= 15 with M = 17 / 18 / >= 19, or a truncated match
+// M = 1..3 whatever L, LZ4.c:317 + :540-544) is resolved by a per-lane LDS
+// stack of choice points: the plain reading is taken first and undone if the
+// block does not then end exactly at its last byte with 300 decoded bytes
+// (or 1..300 for the last block) and size fields summing to the block
+// header's (LZ4.c:617).  A plain reading of such a token decodes >= 32
+// bytes, so at most 9 choice points are ever pending; a backtrack rewrites
+// the tail.  A sequence's size field equals the bytes it occupies, plus one
+// for a truncated reading, so the running sum is (ip - 3) + #truncated.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,43 +47,90 @@ constexpr int kBlk = LZ4R_BLOCK;
 constexpr int kInMax = LZ4R_BLOCK_BOUND;   // bytes of one encoded block (bound)
 constexpr int kLanes = 64;                 // blocks per workgroup (one wave)
 constexpr int kDepth = 10;                 // choice points per lane (<= 9 needed)
-constexpr int kMaxSteps = 1 << 16;         // parse budget: a hostile stream cannot spin a lane
+constexpr int kMaxSteps = 1 << 16;         // header budget: a hostile stream cannot spin a lane
+
+typedef uint64_t u64u __attribute__((aligned(1)));
+typedef uint32_t u32u __attribute__((aligned(1)));
+typedef uint16_t u16u __attribute__((aligned(1)));
 
 struct DecLds {
-  alignas(16) uint8_t out[kLanes * kBlk];  // lane l's block at out[300 l]
-  uint64_t stk[kDepth][kLanes];            // choice points, column per lane
-  uint32_t qlen[kLanes];                   // decoded bytes per block (0 = failed)
+  alignas(16) uint8_t out[kLanes * kBlk + 32];   // lane l's block at out[300 l] (+ read slack)
+  uint32_t stk[kDepth][kLanes];                  // choice points, column per lane
+  uint32_t qlen[kLanes];                         // decoded bytes per block (0 = failed)
 };
 
-__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
-  return __builtin_amdgcn_alignbyte(hi, lo, s);
-}
+struct V16 {
+  uint64_t lo, hi;
+};
 
-// Bytes a .. a+7 after p, little-endian; `avail` = readable bytes after p.
-__device__ __forceinline__ uint64_t ld8(const uint8_t *p, int a, int avail) {
-  const uint8_t *q = p + a;
-  if (a + 12 <= avail) {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)q & ~(uintptr_t)3);
-    const uint32_t s = (uint32_t)((uintptr_t)q & 3);
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-    return funnel(w1, w0, s) | ((uint64_t)funnel(w2, w1, s) << 32);
-  }
-  uint64_t r = 0;
-  for (int t = 0; t < 8; ++t)
-    if (a + t < avail) r |= (uint64_t)q[t] << (8 * t);
-  return r;
-}
+// The lane's encoded block in global memory; `avail` = readable bytes from p.
+struct Bytes {
+  const uint8_t *p;
+  size_t avail;
 
-__device__ __forceinline__ uint32_t ld4(const uint8_t *p, int a, int avail) {
-  const uint8_t *q = p + a;
-  if (a + 8 <= avail) {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)q & ~(uintptr_t)3);
-    return funnel(w[1], w[0], (uint32_t)((uintptr_t)q & 3));
+  __device__ __forceinline__ uint64_t ld8(int a) const {
+    if ((size_t)a + 8 <= avail) return *reinterpret_cast<const u64u *>(p + a);
+    uint64_t r = 0;
+    for (int t = 0; t < 8; ++t)
+      if ((size_t)(a + t) < avail) r |= (uint64_t)p[a + t] << (8 * t);
+    return r;
   }
-  uint32_t r = 0;
-  for (int t = 0; t < 4; ++t)
-    if (a + t < avail) r |= (uint32_t)q[t] << (8 * t);
-  return r;
+  __device__ __forceinline__ V16 ld16(int a) const {
+    if ((size_t)a + 16 <= avail) {
+      const u64u *q = reinterpret_cast<const u64u *>(p + a);
+      return {q[0], q[1]};
+    }
+    return {ld8(a), ld8(a + 8)};
+  }
+};
+
+// The lane's 300-byte output slot in LDS.  Reads may run past the slot
+// (into a neighbour or the slack) and are masked by the caller; writes are
+// exact.
+struct Slot {
+  uint8_t *o;
+
+  __device__ __forceinline__ uint64_t ld8(int a) const {
+    return *reinterpret_cast<const u64u *>(o + a);
+  }
+  __device__ __forceinline__ V16 ld16(int a) const {
+    const u64u *q = reinterpret_cast<const u64u *>(o + a);
+    return {q[0], q[1]};
+  }
+  // the first n (1..16) bytes of v at o[a]
+  __device__ __forceinline__ void st(int a, V16 v, int n) const {
+    if (n == 16) {
+      *reinterpret_cast<u64u *>(o + a) = v.lo;
+      *reinterpret_cast<u64u *>(o + a + 8) = v.hi;
+      return;
+    }
+    uint64_t w = v.lo;
+    if (n & 8) {
+      *reinterpret_cast<u64u *>(o + a) = w;
+      a += 8;
+      w = v.hi;
+    }
+    if (n & 4) {
+      *reinterpret_cast<u32u *>(o + a) = (uint32_t)w;
+      a += 4;
+      w >>= 32;
+    }
+    if (n & 2) {
+      *reinterpret_cast<u16u *>(o + a) = (uint16_t)w;
+      a += 2;
+      w >>= 16;
+    }
+    if (n & 1) o[a] = (uint8_t)w;
+  }
+};
+
+// the low D (1..7) bytes of w repeated over 8 bytes
+__device__ __forceinline__ uint64_t replicate(uint64_t w, int D) {
+  uint64_t x = w & ((1ull << (8 * D)) - 1);
+  x |= x << (8 * D);
+  if (2 * D < 8) x |= x << (16 * D);
+  if (4 * D < 8) x |= x << (32 * D);
+  return x;
 }
 
 __device__ __forceinline__ int litext_len(int L) {
@@ -82,58 +138,24 @@ __device__ __forceinline__ int litext_len(int L) {
   return ((L - 15) & 255) == 255 ? 2 : 1;
 }
 
-__device__ __forceinline__ bool litext_ok(int ip0, int len, int e0, int e1, int L) {
-  const int r = (L - 15) & 255;
-  return r == 255 ? (ip0 + 1 < len && e0 == 255 && e1 == 0) : (ip0 < len && e0 == r);
-}
-
-// One reading of the sequence at ip (output position pos) whose first eight
-// bytes are h.  alt 0: the token's nibbles as written for M == 0 or M >= 4;
-// alt 1..3: a truncated match M = alt, tokens 0xFD..0xFF only, size field
-// S = L + 5 + litext_len(L) + 1 (LZ4.c:569-575).
-__device__ __forceinline__ bool read_seq(const uint8_t *p, int avail, int len, int ip,
-                                         uint64_t h, int pos, bool last, int alt, int &L,
-                                         int &M, int &D, int &lit, int &nip) {
-  const int tok = (int)(h & 255), Sz = (int)((h >> 8) & 0xFFFF);
-  const int e0 = (int)((h >> 24) & 255), e1 = (int)((h >> 32) & 255);
+// Truncated reading of the sequence at ip: match length M = alt in 1..3
+// (tokens 0xFD..0xFF only); size field S = L + 5 + litext_len(L) + 1
+// (LZ4.c:569-575).  e0, e1 = the two bytes after the size field.
+__device__ bool read_truncated(const Bytes &p, int len, int ip, int Sz, int e0, int e1, int pos,
+                               int alt, int &L, int &M, int &D, int &lit, int &nip) {
   const int ip0 = ip + 3;
-  if (alt == 0) {
-    const int tl = tok >> 4, tm = tok & 15, mx = tm == 15 ? 1 : 0;
-    int le = 0;
-    if (tl == 15) {
-      le = (ip0 < len && e0 == 255) ? 2 : 1;
-      L = Sz - 5 - le - mx;
-      if (L < 15 || litext_len(L) != le || !litext_ok(ip0, len, e0, e1, L)) return false;
-    } else {
-      L = tl;
-      if (Sz != L + 5 + mx) return false;
-    }
-    lit = ip0 + le;
-    if (lit + L + 2 > len || pos + L > kBlk) return false;
-    const uint32_t t = ld4(p, lit + L, avail);
-    D = (int)(t & 0xFFFF);
-    nip = lit + L + 2;
-    if (D == 0) {                            // literal-only tail (LZ4.c:585-613)
-      M = 0;
-      return last && tm == 0;
-    }
-    if (tm == 15) {
-      if (nip >= len) return false;
-      M = 19 + (int)((t >> 16) & 255);
-      ++nip;
-    } else {
-      M = tm + 4;
-    }
-    return D <= pos + L && pos + L + M <= kBlk;
-  }
   M = alt;
   for (int le = 0; le <= 2; ++le) {
     L = Sz - 6 - le;
     if (L < 0 || litext_len(L) != le) continue;
-    if (le && !litext_ok(ip0, len, e0, e1, L)) continue;
+    if (le) {
+      const int r = (L - 15) & 255;
+      const bool ok = r == 255 ? (ip0 + 1 < len && e0 == 255 && e1 == 0) : (ip0 < len && e0 == r);
+      if (!ok) continue;
+    }
     lit = ip0 + le;
     if (lit + L + 2 > len || pos + L + M > kBlk) continue;
-    D = (int)(ld4(p, lit + L, avail) & 0xFFFF);
+    D = (int)(p.ld8(lit + L) & 0xFFFF);
     if (D == 0 || D > pos + L) continue;
     nip = lit + L + 2;
     return true;
@@ -141,62 +163,107 @@ __device__ __forceinline__ bool read_seq(const uint8_t *p, int avail, int len, i
   return false;
 }
 
+// choice point: k 8 | ip 11 | pos 9 | #truncated 2 | next reading 2
+__device__ __forceinline__ uint32_t pack_choice(int k, int ip, int pos, int ntr, int alt) {
+  return (uint32_t)k | ((uint32_t)ip << 8) | ((uint32_t)pos << 19) | ((uint32_t)ntr << 28) |
+         ((uint32_t)alt << 30);
+}
+
 // literals p[lit, lit+L) -> o[pos, pos+L)
-__device__ __forceinline__ void emit_literals(uint8_t *o, int pos, const uint8_t *p, int lit,
-                                              int L, int avail) {
-  int i = 0;
-  for (; i + 8 <= L; i += 8) {
-    const uint64_t w = ld8(p, lit + i, avail);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) o[pos + i + t] = (uint8_t)(w >> (8 * t));
+__device__ __forceinline__ void copy_literals(const Slot &o, int pos, const Bytes &p, int lit,
+                                              int L) {
+  for (int i = 0; i < L; i += 16) o.st(pos + i, p.ld16(lit + i), L - i < 16 ? L - i : 16);
+}
+
+// o[q + i] = o[q - D + i] for i < M, in order (D-periodic when D < M)
+__device__ __forceinline__ void copy_match(const Slot &o, int q, int D, int M) {
+  int i = 0, d = D;
+  if (D < 8) {                                   // seed: whole periods within 8 bytes
+    const uint64_t x = replicate(o.ld8(q - D), D);
+    const int per = 8 - 8 % D;
+    i = M < per ? M : per;
+    o.st(q, {x, 0}, i);
+    d = i + D - i % D;                           // multiple of D, <= i + D
   }
-  if (i < L) {
-    const uint64_t w = ld8(p, lit + i, avail);
-    for (int t = 0; i + t < L; ++t) o[pos + i + t] = (uint8_t)(w >> (8 * t));
+  while (i < M) {
+    int n = M - i < 16 ? M - i : 16;
+    if (n > d) n = d;
+    o.st(q + i, o.ld16(q + i - d), n);
+    i += n;
+    if (d < 16) d = i + D - i % D;               // grow while short
   }
 }
 
-// match of length M at distance D: o[q + i] = o[q - D + i] in order, i.e.
-// periodic with period D when D < M
-__device__ __forceinline__ void emit_match(uint8_t *o, int q, int D, int M) {
-  if (D >= 8) {
-    int i = 0;
-    for (; i + 8 <= M; i += 8) {
-      uint8_t c[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) c[t] = o[q - D + i + t];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) o[q + i + t] = c[t];
+// Decode one block into its slot.  Returns the decoded length, or 0 if the
+// block is malformed.
+__device__ __forceinline__ int decode_block(const Bytes &p, int len, bool last, const Slot &o,
+                                            uint32_t (*stk)[kLanes], int lane) {
+  const uint64_t h0 = p.ld8(0);
+  const int nseq = (int)(h0 & 255);                  // nseq & 0xFF; <= 76 in practice
+  const int want = (int)((h0 >> 8) & 0xFFFF) - 3;    // LZ4.c:617
+  if (len < 3 || nseq == 0 || want < 0) return 0;
+  int k = 0, ip = 3, pos = 0, ntr = 0, nch = 0, alt = 0, steps = 0;
+  for (;;) {
+    bool ok = false;
+    int L = 0, M = 0, D = 0, lit = 0, nip = 0;
+    if (++steps > kMaxSteps) return 0;
+    if (k == nseq) {
+      if (ip == len && ip - 3 + ntr == want && (pos == kBlk || (last && pos >= 1))) return pos;
+    } else if (ip + 3 <= len) {
+      const uint64_t h = p.ld8(ip);
+      const int tok = (int)(h & 255), Sz = (int)((h >> 8) & 0xFFFF);
+      const int e0 = (int)((h >> 24) & 255), e1 = (int)((h >> 32) & 255);
+      const bool fits = ip - 3 + ntr + Sz <= want;
+      if (alt == 0) {
+        // plain reading, branch-free: token nibbles as written (M == 0 or M >= 4)
+        const int tl = tok >> 4, tm = tok & 15;
+        const int mx = tm == 15 ? 1 : 0;
+        const bool big = tl == 15;
+        const int le = big ? (e0 == 255 ? 2 : 1) : 0;
+        L = big ? Sz - 5 - le - mx : tl;
+        const int r = (L - 15) & 255;
+        bool okp = big ? (L >= 15 && (e0 == 255 ? (r == 255 && e1 == 0) : r == e0))
+                       : Sz == L + 5 + mx;
+        lit = ip + 3 + le;
+        okp = okp && fits && lit + L + 2 <= len && pos + L <= kBlk;
+        const uint32_t t = (uint32_t)p.ld8(okp ? lit + L : 0);
+        D = (int)(t & 0xFFFF);
+        const bool hasm = D != 0;
+        M = hasm ? (mx ? 19 + (int)((t >> 16) & 255) : tm + 4) : 0;
+        nip = lit + L + 2 + (hasm ? mx : 0);
+        okp = okp && (hasm ? (nip <= len && D <= pos + L && pos + L + M <= kBlk)
+                           : (k + 1 == nseq && tm == 0));   // literal-only tail, LZ4.c:585-613
+        ok = okp;
+        if (tok >= 0xFD) {
+          if (okp) {                                 // the truncated reading remains
+            if (nch == kDepth) return 0;
+            stk[nch++][lane] = pack_choice(k, ip, pos, ntr, tok - 0xFC);
+          } else {
+            alt = tok - 0xFC;
+          }
+        }
+      }
+      if (alt != 0) {                                // truncated reading (rare)
+        ok = fits && ntr < 3 &&
+             read_truncated(p, len, ip, Sz, e0, e1, pos, alt, L, M, D, lit, nip);
+        ntr += ok ? 1 : 0;
+      }
     }
-    for (; i < M; ++i) o[q + i] = o[q - D + i];
-  } else {
-    // period D < 8: X = the period repeated over 16 bytes (lo, hi); the
-    // 8 bytes at q + i are X[s .. s+8) with s = i mod D
-    uint64_t pat = 0;
-    for (int t = 0; t < D; ++t) pat |= (uint64_t)o[q - D + t] << (8 * t);
-    uint64_t lo = 0, hi = 0;
-    int r = 0;
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const uint64_t c = (pat >> (8 * r)) & 255;
-      if (t < 8) lo |= c << (8 * t);
-      else hi |= c << (8 * (t - 8));
-      r = r + 1 == D ? 0 : r + 1;
+    if (ok) {
+      copy_literals(o, pos, p, lit, L);
+      if (M) copy_match(o, pos + L, D, M);
+      ++k;
+      ip = nip;
+      pos += L + M;
+      alt = 0;
+      continue;
     }
-    int s = 0;
-    for (int i = 0; i < M; i += 8) {
-      const uint64_t w = s ? (lo >> (8 * s)) | (hi << (64 - 8 * s)) : lo;
-      const int n = M - i < 8 ? M - i : 8;
-      for (int t = 0; t < n; ++t) o[q + i + t] = (uint8_t)(w >> (8 * t));
-      s += 8 % D;
-      if (s >= D) s -= D;
-    }
+    // dead end: resume the most recent choice point with its other reading
+    if (nch == 0) return 0;
+    const uint32_t c = stk[--nch][lane];
+    k = (int)(c & 255); ip = (int)((c >> 8) & 2047); pos = (int)((c >> 19) & 511);
+    ntr = (int)((c >> 28) & 3); alt = (int)(c >> 30);
   }
-}
-
-__device__ __forceinline__ uint64_t pack_choice(int k, int ip, int pos, int ssum, int alt) {
-  return (uint64_t)k | ((uint64_t)ip << 8) | ((uint64_t)pos << 24) | ((uint64_t)ssum << 40) |
-         ((uint64_t)alt << 56);
 }
 
 __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
@@ -206,69 +273,20 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
   __shared__ DecLds S;
   const int lane = threadIdx.x;
   const size_t b0 = (size_t)blockIdx.x * kLanes;
+  const int nl = (int)(nb - b0 < (size_t)kLanes ? nb - b0 : kLanes);   // blocks here
   const size_t b = b0 + lane;
-  uint8_t *o = S.out + lane * kBlk;
-  int q = 0;                                       // decoded bytes (0 = failed / absent)
 
-  if (b < nb) {
+  int q = 0;                                         // decoded bytes (0 = failed / absent)
+  if (lane < nl) {
     const bool last = b == nb - 1;
     const size_t beg = 1 + boff[b];
     const size_t end = last ? in_len : 1 + boff[b + 1];
-    bool ok = end >= beg + 3 && end <= in_len && end - beg <= (size_t)kInMax;
-    const uint8_t *p = in + (ok ? beg : 0);
-    const int len = ok ? (int)(end - beg) : 0;
-    const int avail = ok ? (int)(in_len - beg < (size_t)(1 << 30) ? in_len - beg : 1 << 30) : 0;
-    int k = 0, ip = 3, pos = 0, nch = 0, alt = 0, steps = 0, ssum = 0, nseq = 0, want = 0;
-    if (ok) {
-      const uint64_t h0 = ld8(p, 0, avail);
-      nseq = (int)(h0 & 255);                        // nseq & 0xFF; <= 76 in practice
-      want = (int)((h0 >> 8) & 0xFFFF) - 3;          // LZ4.c:617
-      ok = nseq > 0 && want >= 0;
+    if (end >= beg + 3 && end <= in_len && end - beg <= (size_t)kInMax) {
+      const Bytes p{in + beg, in_len - beg};
+      q = decode_block(p, (int)(end - beg), last, Slot{S.out + lane * kBlk}, S.stk, lane);
     }
-    while (ok) {
-      if (++steps > kMaxSteps) { ok = false; break; }
-      if (k == nseq) {
-        if (ip == len && ssum == want && (pos == kBlk || (last && pos >= 1))) break;
-      } else if (ip + 3 <= len) {
-        const uint64_t h = ld8(p, ip, avail);
-        const int tok = (int)(h & 255), Sz = (int)((h >> 8) & 0xFFFF);
-        int L = 0, M = 0, D = 0, lit = 0, nip = 0;
-        bool got = false;
-        if (ssum + Sz <= want && alt <= 3) {
-          got = read_seq(p, avail, len, ip, h, pos, k + 1 == nseq, alt, L, M, D, lit, nip);
-          if (alt == 0 && tok >= 0xFD) {
-            if (got) {                               // the truncated reading remains
-              if (nch == kDepth) { ok = false; break; }
-              S.stk[nch++][lane] = pack_choice(k, ip, pos, ssum, tok - 0xFC);
-            } else {
-              got = read_seq(p, avail, len, ip, h, pos, k + 1 == nseq, tok - 0xFC, L, M, D,
-                             lit, nip);
-            }
-          }
-        }
-        if (got) {
-          emit_literals(o, pos, p, lit, L, avail);
-          emit_match(o, pos + L, D, M);
-          ++k;
-          ssum += Sz;
-          ip = nip;
-          pos += L + M;
-          alt = 0;
-          continue;
-        }
-      }
-      // dead end: resume the most recent choice point with its other reading
-      if (nch == 0) { ok = false; break; }
-      const uint64_t c = S.stk[--nch][lane];
-      k = (int)(c & 255); ip = (int)((c >> 8) & 0xFFFF); pos = (int)((c >> 24) & 0xFFFF);
-      ssum = (int)((c >> 40) & 0xFFFF); alt = (int)(c >> 56);
-    }
-    if (ok) {
-      q = pos;
-      if (last) result[0] = (unsigned long long)(b * kBlk + q);
-    } else {
-      atomicMin(&result[1], (unsigned long long)b + 1);
-    }
+    if (q == 0) atomicMin(&result[1], (unsigned long long)b + 1);
+    else if (last) result[0] = (unsigned long long)(b * kBlk + q);
   }
   S.qlen[lane] = (uint32_t)q;
   __syncthreads();
@@ -276,16 +294,9 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
   // ---- store the wave's contiguous output -----------------------------------
   // every block but the last decodes to exactly 300 bytes, so the valid range
   // is [300 b0, 300 b0 + sum q); a failed block leaves garbage (error raised)
-  __shared__ uint32_t s_total;
-  if (lane == 0) {
-    uint32_t t = 0;
-    const int nl = (int)(nb - b0 < (size_t)kLanes ? nb - b0 : kLanes);
-    for (int l = 0; l < nl; ++l) t += l + 1 < nl ? kBlk : S.qlen[l];
-    s_total = t;
-  }
-  __syncthreads();
+  size_t total = 0;
+  for (int l = 0; l < nl; ++l) total += l + 1 < nl ? kBlk : S.qlen[l];
   const size_t o0 = b0 * (size_t)kBlk;
-  size_t total = s_total;
   if (o0 >= out_cap) return;
   if (o0 + total > out_cap) total = out_cap - o0;
   if (((reinterpret_cast<uintptr_t>(out) + o0) & 15) == 0) {

@@ -183,4 +183,7 @@ def decompress_device(d_stream, length, d_offsets, nb, out_cap, d_out=None, stre
     n, bad = (int(x) for x in res.cpu().tolist())
     if bad != -1:
         raise Lz4Error(_lib.LZ4R_ERR_CORRUPT, f"lz4r_decompress_device: block {bad - 1}")
+    if n > out_cap:
+        raise Lz4Error(_lib.LZ4R_ERR_CAPACITY,
+                       f"lz4r_decompress_device: needs {n} bytes, capacity {out_cap}")
     return d_out, n

@@ -123,3 +123,38 @@ def test_full_size_1gib_roundtrip(comp):
     torch.cuda.synchronize()
     assert got == n
     assert torch.equal(d_out[:n], d_in)
+
+
+def test_tight_capacity_and_mixed_inputs(comp):
+    """Output buffers sized exactly to the decoded length (the last slot's
+    8-byte accesses stay inside the capacity) over mixed inputs."""
+    import torch
+    from lz4jpeg import lz4
+    rng = np.random.default_rng(5)
+    parts = [golden_inputs.lz4_input("metamorphosis_spaces"),
+             rng.integers(0, 256, 50_000, dtype=np.uint8).tobytes(),
+             golden_inputs.lz4_input("m_eq_2"), golden_inputs.lz4_input("lit_270")]
+    for data in parts:
+        b = np.frombuffer(data, dtype=np.uint8)
+        d_in = torch.from_numpy(b.copy()).cuda()
+        d_stream, length = comp.compress_device(d_in)
+        nb = (b.size + 299) // 300
+        d_offs = torch.from_numpy(comp.block_offsets(nb).astype(np.int64)).cuda()
+        d_out, got = lz4.decompress_device(d_stream, length, d_offs, nb, b.size)
+        torch.cuda.synchronize()
+        assert got == b.size
+        assert torch.equal(d_out[:b.size], d_in)
+
+
+def test_capacity_too_small_reported(comp):
+    import torch
+    from lz4jpeg import lz4
+    data = golden_inputs.lz4_input("text_10000")
+    b = np.frombuffer(data, dtype=np.uint8)
+    d_in = torch.from_numpy(b.copy()).cuda()
+    d_stream, length = comp.compress_device(d_in)
+    nb = (b.size + 299) // 300
+    d_offs = torch.from_numpy(comp.block_offsets(nb).astype(np.int64)).cuda()
+    with pytest.raises(lz4.Lz4Error) as ei:
+        lz4.decompress_device(d_stream, length, d_offs, nb, b.size - 1)
+    assert ei.value.code == -3
