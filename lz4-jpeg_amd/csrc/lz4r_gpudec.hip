@@ -12,7 +12,7 @@
 // Mapping: one LANE per block, 64 consecutive blocks per wave (a wave per
 // block would issue every serial parsing step as a full wave instruction).
 // The walk is latency- and issue-bound, so the kernel keeps LDS small for
-// occupancy (22 KB per wave: the 64 output slots + the choice stack) and
+// occupancy (19.5 KB of LDS per wave: the 64 output slots) and
 // keeps instruction counts low:
 //   - the lane reads its encoded bytes with single unaligned 8/16-byte
 //     global loads (L1/L2 absorb the re-reads of the wave's ~20 KB range);
@@ -23,13 +23,15 @@
 //     match is D-periodic, so any multiple of D up to the bytes already
 //     written + D is a valid distance), with D < 8 seeded by replicating
 //     its period over 8 bytes;
-//   - stores into the LDS slot are exact-size (b64/b32/b16/b8 pieces, the
-//     hardware runs in unaligned mode), so no lane touches a neighbour's slot;
+//   - stores into the LDS slot are unaligned 16-byte stores (the hardware
+//     runs in unaligned mode) whose bytes past the wanted ones fall beyond
+//     the lane's write frontier; within 16 bytes of the slot end they are
+//     exact-size (b64/b32/b16/b8 pieces), so no lane touches a neighbour;
 //   - the wave's 64 x 300 = 19200 contiguous bytes leave as 16-B stores.
 // L comes from the exact u16 size field; the one ambiguous token family
 // (0xFD..0xFF: L >= 15 with M = 17 / 18 / >= 19, or a truncated match
-// M = 1..3 whatever L, LZ4.c:317 + :540-544) is resolved by a per-lane LDS
-// stack of choice points: the plain reading is taken first and undone if the
+// M = 1..3 whatever L, LZ4.c:317 + :540-544) is resolved by a per-lane
+// stack of choice points (registers): the plain reading is taken first and undone if the
 // block does not then end exactly at its last byte with 300 decoded bytes
 // (or 1..300 for the last block) and size fields summing to the block
 // header's (LZ4.c:617).  A plain reading of such a token decodes >= 32
@@ -54,8 +56,7 @@ typedef uint32_t u32u __attribute__((aligned(1)));
 typedef uint16_t u16u __attribute__((aligned(1)));
 
 struct DecLds {
-  alignas(16) uint8_t out[kLanes * kBlk + 32];   // lane l's block at out[300 l] (+ read slack)
-  uint32_t stk[kDepth][kLanes];                  // choice points, column per lane
+  alignas(16) uint8_t out[kLanes * kBlk + 32];   // lane l's block at out[300 l] (+ slack)
   uint32_t qlen[kLanes];                         // decoded bytes per block (0 = failed)
 };
 
@@ -64,19 +65,22 @@ struct V16 {
 };
 
 // The lane's encoded block in global memory; `avail` = readable bytes from p.
+// kSafe: bounds-checked (only the wave holding the stream's last bytes needs
+// it; everywhere else a 16-byte read past a block stays inside the stream).
+template <bool kSafe>
 struct Bytes {
   const uint8_t *p;
   size_t avail;
 
   __device__ __forceinline__ uint64_t ld8(int a) const {
-    if ((size_t)a + 8 <= avail) return *reinterpret_cast<const u64u *>(p + a);
+    if (!kSafe || (size_t)a + 8 <= avail) return *reinterpret_cast<const u64u *>(p + a);
     uint64_t r = 0;
     for (int t = 0; t < 8; ++t)
       if ((size_t)(a + t) < avail) r |= (uint64_t)p[a + t] << (8 * t);
     return r;
   }
   __device__ __forceinline__ V16 ld16(int a) const {
-    if ((size_t)a + 16 <= avail) {
+    if (!kSafe || (size_t)a + 16 <= avail) {
       const u64u *q = reinterpret_cast<const u64u *>(p + a);
       return {q[0], q[1]};
     }
@@ -96,6 +100,18 @@ struct Slot {
   __device__ __forceinline__ V16 ld16(int a) const {
     const u64u *q = reinterpret_cast<const u64u *>(o + a);
     return {q[0], q[1]};
+  }
+  // v at o[a .. a+16) when that stays inside the slot, else exactly n bytes.
+  // Bytes past the n meant ones land beyond the lane's write frontier and
+  // are overwritten before anything reads them (output is produced in
+  // order; a backtrack rewrites from the choice point on).
+  __device__ __forceinline__ void st_fast(int a, V16 v, int n) const {
+    if (a + 16 <= kBlk) {
+      *reinterpret_cast<u64u *>(o + a) = v.lo;
+      *reinterpret_cast<u64u *>(o + a + 8) = v.hi;
+    } else {
+      st(a, v, n);
+    }
   }
   // the first n (1..16) bytes of v at o[a]
   __device__ __forceinline__ void st(int a, V16 v, int n) const {
@@ -133,6 +149,14 @@ __device__ __forceinline__ uint64_t replicate(uint64_t w, int D) {
   return x;
 }
 
+// v >> (8 * nbytes), nbytes in 0..15
+__device__ __forceinline__ V16 shr_bytes(V16 v, int nbytes) {
+  const int s = 8 * nbytes;
+  if (s == 0) return v;
+  if (s < 64) return {(v.lo >> s) | (v.hi << (64 - s)), v.hi >> s};
+  return {v.hi >> (s - 64), 0};
+}
+
 __device__ __forceinline__ int litext_len(int L) {
   if (L < 15) return 0;
   return ((L - 15) & 255) == 255 ? 2 : 1;
@@ -141,7 +165,8 @@ __device__ __forceinline__ int litext_len(int L) {
 // Truncated reading of the sequence at ip: match length M = alt in 1..3
 // (tokens 0xFD..0xFF only); size field S = L + 5 + litext_len(L) + 1
 // (LZ4.c:569-575).  e0, e1 = the two bytes after the size field.
-__device__ bool read_truncated(const Bytes &p, int len, int ip, int Sz, int e0, int e1, int pos,
+template <typename BytesT>
+__device__ bool read_truncated(const BytesT &p, int len, int ip, int Sz, int e0, int e1, int pos,
                                int alt, int &L, int &M, int &D, int &lit, int &nip) {
   const int ip0 = ip + 3;
   M = alt;
@@ -169,10 +194,15 @@ __device__ __forceinline__ uint32_t pack_choice(int k, int ip, int pos, int ntr,
          ((uint32_t)alt << 30);
 }
 
-// literals p[lit, lit+L) -> o[pos, pos+L)
-__device__ __forceinline__ void copy_literals(const Slot &o, int pos, const Bytes &p, int lit,
+// literals p[lit, lit+L) -> o[pos, pos+L), 32 bytes per step
+template <typename BytesT>
+__device__ __forceinline__ void copy_literals(const Slot &o, int pos, const BytesT &p, int lit,
                                               int L) {
-  for (int i = 0; i < L; i += 16) o.st(pos + i, p.ld16(lit + i), L - i < 16 ? L - i : 16);
+  for (int i = 0; i < L; i += 32) {
+    const V16 a = p.ld16(lit + i), b = p.ld16(lit + i + 16);
+    o.st_fast(pos + i, a, L - i < 16 ? L - i : 16);
+    if (i + 16 < L) o.st_fast(pos + i + 16, b, L - i - 16 < 16 ? L - i - 16 : 16);
+  }
 }
 
 // o[q + i] = o[q - D + i] for i < M, in order (D-periodic when D < M)
@@ -182,37 +212,44 @@ __device__ __forceinline__ void copy_match(const Slot &o, int q, int D, int M) {
     const uint64_t x = replicate(o.ld8(q - D), D);
     const int per = 8 - 8 % D;
     i = M < per ? M : per;
-    o.st(q, {x, 0}, i);
+    o.st_fast(q, {x, x}, i);
     d = i + D - i % D;                           // multiple of D, <= i + D
   }
   while (i < M) {
     int n = M - i < 16 ? M - i : 16;
     if (n > d) n = d;
-    o.st(q + i, o.ld16(q + i - d), n);
+    o.st_fast(q + i, o.ld16(q + i - d), n);
     i += n;
     if (d < 16) d = i + D - i % D;               // grow while short
   }
 }
 
 // Decode one block into its slot.  Returns the decoded length, or 0 if the
-// block is malformed.
-__device__ __forceinline__ int decode_block(const Bytes &p, int len, bool last, const Slot &o,
-                                            uint32_t (*stk)[kLanes], int lane) {
+// block is malformed.  Each sequence is decoded from a 16-byte window h of
+// the stream at ip; its distance bytes and literals come from the window
+// when they lie inside it, and the next sequence's window is requested as
+// soon as the next ip is known (it does not depend on the distance: the
+// literal-only tail has tm = 0, so no match-extension byte either way), so
+// its load overlaps this sequence's copies.
+template <typename BytesT>
+__device__ __forceinline__ int decode_block(const BytesT &p, int len, bool last, const Slot &o) {
+  uint32_t stk[kDepth];                              // choice points (registers; rare)
   const uint64_t h0 = p.ld8(0);
   const int nseq = (int)(h0 & 255);                  // nseq & 0xFF; <= 76 in practice
   const int want = (int)((h0 >> 8) & 0xFFFF) - 3;    // LZ4.c:617
   if (len < 3 || nseq == 0 || want < 0) return 0;
   int k = 0, ip = 3, pos = 0, ntr = 0, nch = 0, alt = 0, steps = 0;
+  V16 h = p.ld16(3);
   for (;;) {
     bool ok = false;
     int L = 0, M = 0, D = 0, lit = 0, nip = 0;
+    V16 hn = {0, 0};
     if (++steps > kMaxSteps) return 0;
     if (k == nseq) {
       if (ip == len && ip - 3 + ntr == want && (pos == kBlk || (last && pos >= 1))) return pos;
     } else if (ip + 3 <= len) {
-      const uint64_t h = p.ld8(ip);
-      const int tok = (int)(h & 255), Sz = (int)((h >> 8) & 0xFFFF);
-      const int e0 = (int)((h >> 24) & 255), e1 = (int)((h >> 32) & 255);
+      const int tok = (int)(h.lo & 255), Sz = (int)((h.lo >> 8) & 0xFFFF);
+      const int e0 = (int)((h.lo >> 24) & 255), e1 = (int)((h.lo >> 32) & 255);
       const bool fits = ip - 3 + ntr + Sz <= want;
       if (alt == 0) {
         // plain reading, branch-free: token nibbles as written (M == 0 or M >= 4)
@@ -226,18 +263,21 @@ __device__ __forceinline__ int decode_block(const Bytes &p, int len, bool last, 
                        : Sz == L + 5 + mx;
         lit = ip + 3 + le;
         okp = okp && fits && lit + L + 2 <= len && pos + L <= kBlk;
-        const uint32_t t = (uint32_t)p.ld8(okp ? lit + L : 0);
+        nip = lit + L + 2 + mx;
+        hn = p.ld16(okp ? nip : ip);                 // next window, in flight during the copies
+        const int off = lit + L - ip;                // distance bytes within the window?
+        const uint32_t t = off + 3 <= 16 ? (uint32_t)shr_bytes(h, off).lo
+                                         : (uint32_t)p.ld8(okp ? lit + L : 0);
         D = (int)(t & 0xFFFF);
         const bool hasm = D != 0;
         M = hasm ? (mx ? 19 + (int)((t >> 16) & 255) : tm + 4) : 0;
-        nip = lit + L + 2 + (hasm ? mx : 0);
         okp = okp && (hasm ? (nip <= len && D <= pos + L && pos + L + M <= kBlk)
                            : (k + 1 == nseq && tm == 0));   // literal-only tail, LZ4.c:585-613
         ok = okp;
         if (tok >= 0xFD) {
           if (okp) {                                 // the truncated reading remains
             if (nch == kDepth) return 0;
-            stk[nch++][lane] = pack_choice(k, ip, pos, ntr, tok - 0xFC);
+            stk[nch++] = pack_choice(k, ip, pos, ntr, tok - 0xFC);
           } else {
             alt = tok - 0xFC;
           }
@@ -247,22 +287,29 @@ __device__ __forceinline__ int decode_block(const Bytes &p, int len, bool last, 
         ok = fits && ntr < 3 &&
              read_truncated(p, len, ip, Sz, e0, e1, pos, alt, L, M, D, lit, nip);
         ntr += ok ? 1 : 0;
+        if (ok) hn = p.ld16(nip);
       }
     }
     if (ok) {
-      copy_literals(o, pos, p, lit, L);
+      if (lit + L <= ip + 16) {                      // literals inside the window
+        if (L) o.st_fast(pos, shr_bytes(h, lit - ip), L);
+      } else {
+        copy_literals(o, pos, p, lit, L);
+      }
       if (M) copy_match(o, pos + L, D, M);
       ++k;
       ip = nip;
+      h = hn;
       pos += L + M;
       alt = 0;
       continue;
     }
     // dead end: resume the most recent choice point with its other reading
     if (nch == 0) return 0;
-    const uint32_t c = stk[--nch][lane];
+    const uint32_t c = stk[--nch];
     k = (int)(c & 255); ip = (int)((c >> 8) & 2047); pos = (int)((c >> 19) & 511);
     ntr = (int)((c >> 28) & 3); alt = (int)(c >> 30);
+    h = p.ld16(ip);
   }
 }
 
@@ -282,8 +329,12 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
     const size_t beg = 1 + boff[b];
     const size_t end = last ? in_len : 1 + boff[b + 1];
     if (end >= beg + 3 && end <= in_len && end - beg <= (size_t)kInMax) {
-      const Bytes p{in + beg, in_len - beg};
-      q = decode_block(p, (int)(end - beg), last, Slot{S.out + lane * kBlk}, S.stk, lane);
+      const Slot o{S.out + lane * kBlk};
+      // a read reaches at most kInMax + 32 bytes past the wave's first block
+      if (1 + boff[b0] + (size_t)(kLanes + 1) * kInMax + 64 <= in_len)
+        q = decode_block(Bytes<false>{in + beg, in_len - beg}, (int)(end - beg), last, o);
+      else
+        q = decode_block(Bytes<true>{in + beg, in_len - beg}, (int)(end - beg), last, o);
     }
     if (q == 0) atomicMin(&result[1], (unsigned long long)b + 1);
     else if (last) result[0] = (unsigned long long)(b * kBlk + q);
