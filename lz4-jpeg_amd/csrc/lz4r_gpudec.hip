@@ -12,7 +12,7 @@
 // Mapping: one LANE per block, 64 consecutive blocks per wave (a wave per
 // block would issue every serial parsing step as a full wave instruction).
 // The walk is latency- and issue-bound, so the kernel keeps LDS small for
-// occupancy (19.5 KB of LDS per wave: the 64 output slots) and
+// occupancy (19.5 KB of LDS per wave: the 64 output slots; 8 waves/CU) and
 // keeps instruction counts low:
 //   - the lane reads its encoded bytes with single unaligned 8/16-byte
 //     global loads (L1/L2 absorb the re-reads of the wave's ~20 KB range);
@@ -28,6 +28,11 @@
 //     the lane's write frontier; within 16 bytes of the slot end they are
 //     exact-size (b64/b32/b16/b8 pieces), so no lane touches a neighbour;
 //   - the wave's 64 x 300 = 19200 contiguous bytes leave as 16-B stores.
+// Measured alternatives that lost (1 GiB text, MI355X): one wave per block
+// (15.5 ms), nested copy loops with byte stores (3.4 ms), staging the wave's
+// input in LDS (halves occupancy: 2x slower), output slots in global memory
+// (read-after-write through L2: 2.4x slower), a one-chunk-per-step state
+// machine (the header path then runs every step: 2x slower).
 // L comes from the exact u16 size field; the one ambiguous token family
 // (0xFD..0xFF: L >= 15 with M = 17 / 18 / >= 19, or a truncated match
 // M = 1..3 whatever L, LZ4.c:317 + :540-544) is resolved by a per-lane
@@ -195,8 +200,8 @@ __device__ __forceinline__ uint32_t pack_choice(int k, int ip, int pos, int ntr,
 }
 
 // literals p[lit, lit+L) -> o[pos, pos+L), 32 bytes per step
-template <typename BytesT>
-__device__ __forceinline__ void copy_literals(const Slot &o, int pos, const BytesT &p, int lit,
+template <typename SlotT, typename BytesT>
+__device__ __forceinline__ void copy_literals(const SlotT &o, int pos, const BytesT &p, int lit,
                                               int L) {
   for (int i = 0; i < L; i += 32) {
     const V16 a = p.ld16(lit + i), b = p.ld16(lit + i + 16);
@@ -206,7 +211,8 @@ __device__ __forceinline__ void copy_literals(const Slot &o, int pos, const Byte
 }
 
 // o[q + i] = o[q - D + i] for i < M, in order (D-periodic when D < M)
-__device__ __forceinline__ void copy_match(const Slot &o, int q, int D, int M) {
+template <typename SlotT>
+__device__ __forceinline__ void copy_match(const SlotT &o, int q, int D, int M) {
   int i = 0, d = D;
   if (D < 8) {                                   // seed: whole periods within 8 bytes
     const uint64_t x = replicate(o.ld8(q - D), D);
@@ -231,8 +237,8 @@ __device__ __forceinline__ void copy_match(const Slot &o, int q, int D, int M) {
 // soon as the next ip is known (it does not depend on the distance: the
 // literal-only tail has tm = 0, so no match-extension byte either way), so
 // its load overlaps this sequence's copies.
-template <typename BytesT>
-__device__ __forceinline__ int decode_block(const BytesT &p, int len, bool last, const Slot &o) {
+template <typename BytesT, typename SlotT>
+__device__ __forceinline__ int decode_block(const BytesT &p, int len, bool last, const SlotT &o) {
   uint32_t stk[kDepth];                              // choice points (registers; rare)
   const uint64_t h0 = p.ld8(0);
   const int nseq = (int)(h0 & 255);                  // nseq & 0xFF; <= 76 in practice
