@@ -231,3 +231,50 @@ int ref_jpeg_reconstruct(const unsigned char *rgba, int w, int h, unsigned char 
     free_pixels(rec.pixels, h);
     return 0;
 }
+
+/* The reference's entropy stage on one stream of n zigzagged ints, exactly as
+ * its main loop runs it (JPEG.c:1211-1349): RLE, encode_huffman,
+ * generate_encoded_sequence, decode_huffman written back over the RLE ints,
+ * inverse_RLE.  Returns the RLE ints, the codes[] table (value, length, bits),
+ * the '0'/'1' string packed MSB-first, and the n ints after the round trip.
+ * The sequence buffer is larger than main()'s 1024 / 512 chars so that no
+ * input overflows it here. */
+int ref_jpeg_entropy(const short *zz, int n, int *rle, int *rle_len, int *ncodes,
+                     short *tab_val, unsigned char *tab_len, unsigned long long *tab_code,
+                     unsigned char *bits, int *nbits, short *decoded)
+{
+    double in[64], out[64];
+    for (int i = 0; i < n; i++) in[i] = zz[i];
+    int *enc = NULL;
+    size_t enc_len = 0;
+    RLE(in, (size_t)n, &enc, &enc_len);
+    for (size_t i = 0; i < enc_len; i++) rle[i] = enc[i];
+    *rle_len = (int)enc_len;
+    size_t code_count = 0;
+    Node *root = NULL;
+    HuffmanCode *codes = encode_huffman(enc, enc_len, &code_count, &root);
+    *ncodes = (int)code_count;
+    for (size_t c = 0; c < code_count; c++) {
+        tab_val[c] = (short)(codes[c].value - 1000);
+        tab_len[c] = (unsigned char)strlen(codes[c].code);
+        unsigned long long v = 0;
+        for (const char *p = codes[c].code; *p; p++) v = (v << 1) | (unsigned long long)(*p == '1');
+        tab_code[c] = v;
+    }
+    static char seq[16384];
+    generate_encoded_sequence(enc, enc_len, codes, (int)code_count, seq);
+    int nb = (int)strlen(seq);
+    memset(bits, 0, (size_t)(nb + 7) / 8);
+    for (int i = 0; i < nb; i++)
+        if (seq[i] == '1') bits[i >> 3] |= (unsigned char)(0x80 >> (i & 7));
+    *nbits = nb;
+    size_t dlen = 0;
+    double *dec = decode_huffman(root, seq, &dlen);
+    for (size_t j = 0; j < dlen; j++) enc[j] = (int)dec[j];          /* :1237-1240 */
+    inverse_RLE(enc, out, (size_t)n, enc_len);                        /* :1346 */
+    for (int i = 0; i < n; i++) decoded[i] = (short)out[i];
+    free(dec);
+    free(codes);
+    free(enc);
+    return 0;
+}

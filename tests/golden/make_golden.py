@@ -52,6 +52,50 @@ JPEG_KAT_8X8 = {  # SURVEY.md Appendix A4, literal coefficients of the 8x8 seed-
 }
 
 
+def entropy_streams(o):
+    """Streams (zigzagged ints of one channel of one tile) for the entropy
+    stage: the 8x8 KAT tile, edge cases, random and natural-image tiles."""
+    import numpy as np
+    st = [("kat_Y", JPEG_KAT_8X8["Y"]), ("kat_Cr", JPEG_KAT_8X8["Cr"]),
+          ("kat_Cb", JPEG_KAT_8X8["Cb"]),
+          ("zeros_Y", [0] * 64), ("zeros_C", [0] * 32),
+          ("one_symbol_C", [32] * 32), ("one_symbol_Y", [64] * 64),   # RLE [n, n]: one code, empty
+          ("all_distinct_Y", list(range(-32, 32))), ("all_distinct_C", list(range(100, 132))),
+          ("alternating_Y", [1, -1] * 32), ("runs_Y", sum([[k] * k for k in range(1, 11)], [])[:64]),
+          ("dc_only_Y", [57] + [0] * 63), ("extremes_Y", [-1024, 1016] * 32)]
+    rng = np.random.default_rng(11)
+    coef = o.jpeg_encode(o.rand_image(32, 16, 7)).reshape(-1, 128)
+    for t in range(coef.shape[0]):
+        st += [(f"rand_t{t}_Y", coef[t, :64].tolist()), (f"rand_t{t}_Cr", coef[t, 64:96].tolist()),
+               (f"rand_t{t}_Cb", coef[t, 96:].tolist())]
+    for k in range(12):
+        n = 64 if k % 2 == 0 else 32
+        alpha = int(rng.integers(2, 40))
+        st.append((f"fuzz{k}", (rng.integers(-alpha // 2, alpha // 2 + 1, n)).tolist()))
+    return st
+
+
+def entropy_vectors(o):
+    """Known answers from the reference's own entropy functions (oracle/_ref:
+    RLE, encode_huffman, generate_encoded_sequence, decode_huffman,
+    inverse_RLE); the restatement must agree.  Kept from the previous run
+    when the reference build is absent."""
+    path = os.path.join(HERE, "entropy.json")
+    if oracle_api.ref_jpeg() is None:
+        return json.load(open(path))
+    vecs = []
+    for name, zz in entropy_streams(o):
+        r = oracle_api.ref_entropy(zz)
+        a = oracle_api.entropy(o, zz)
+        assert (a["rle"], a["table"], a["nbits"], a["bits"]) == \
+            (r["rle"], r["table"], r["nbits"], r["bits"]), name
+        assert r["decoded"] == list(zz), name
+        vecs.append({"name": name, "zz": list(zz), "rle_len": len(r["rle"]),
+                     "table": [[v, ln, str(c)] for v, ln, c in r["table"]],
+                     "nbits": r["nbits"], "bits": r["bits"].hex(), "source": "reference-build"})
+    return vecs
+
+
 def md5(b):
     return hashlib.md5(b).hexdigest()
 
@@ -84,10 +128,13 @@ def main():
             assert r.tobytes() == got, "oracle != reference JPEG.c"
             e["rechecked_against_ref_build"] = True
         jpeg.append(e)
+    entropy = entropy_vectors(o)
+    with open(os.path.join(HERE, "entropy.json"), "w") as f:      # one vector per line
+        f.write("[\n" + ",\n".join(json.dumps(v) for v in entropy) + "\n]\n")
     out = {"lz4": lz4, "jpeg": jpeg, "jpeg_kat_8x8": JPEG_KAT_8X8}
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(out, f, indent=1)
-    print(f"wrote {len(lz4)} lz4 + {len(jpeg)} jpeg vectors")
+    print(f"wrote {len(lz4)} lz4 + {len(jpeg)} jpeg + {len(entropy)} entropy vectors")
 
 
 if __name__ == "__main__":

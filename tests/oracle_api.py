@@ -121,3 +121,63 @@ def ref_reconstruct(rgba):
     L.ref_jpeg_reconstruct.argtypes = [_vp, ctypes.c_int, ctypes.c_int, _vp]
     L.ref_jpeg_reconstruct(a.ctypes.data_as(_vp), w, h, out.ctypes.data_as(_vp))
     return out
+
+
+def _entropy_call(fn, zz, with_decoded):
+    """Shared marshalling of jo_entropy_stream / ref_jpeg_entropy."""
+    zz = np.ascontiguousarray(zz, dtype=np.int16)
+    n = zz.size
+    rle = np.zeros(256, np.int32)
+    rle_len, ncodes, nbits = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    tv = np.zeros(256, np.int16)
+    tl = np.zeros(256, np.uint8)
+    tc = np.zeros(256, np.uint64)
+    bits = np.zeros(2048, np.uint8)
+    dec = np.zeros(64, np.int16)
+    args = [zz.ctypes.data_as(_vp), n, rle.ctypes.data_as(_vp), ctypes.byref(rle_len),
+            ctypes.byref(ncodes), tv.ctypes.data_as(_vp), tl.ctypes.data_as(_vp),
+            tc.ctypes.data_as(_vp), bits.ctypes.data_as(_vp)]
+    if with_decoded:
+        rc = fn(*args, ctypes.byref(nbits), dec.ctypes.data_as(_vp))
+    else:
+        rc = fn(*args, 16384, ctypes.byref(nbits))
+    k = ncodes.value
+    out = {"rc": rc, "rle": rle[:rle_len.value].tolist(),
+           "table": list(zip(tv[:k].tolist(), tl[:k].tolist(), tc[:k].tolist())),
+           "nbits": nbits.value, "bits": bits[:(nbits.value + 7) // 8].tobytes()}
+    if with_decoded:
+        out["decoded"] = dec[:n].tolist()
+    return out
+
+
+def entropy(oracle, zz):
+    """Oracle restatement of the entropy stage for one stream."""
+    fn = oracle.L.jo_entropy_stream
+    fn.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _vp]
+    return _entropy_call(fn, zz, False)
+
+
+def entropy_decode(oracle, e, n):
+    """Oracle decode of an entropy record back to n ints."""
+    fn = oracle.L.jo_entropy_decode
+    fn.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, _vp]
+    k = len(e["table"])
+    tv = np.array([t[0] for t in e["table"]] or [0], np.int16)
+    tl = np.array([t[1] for t in e["table"]] or [0], np.uint8)
+    tc = np.array([t[2] for t in e["table"]] or [0], np.uint64)
+    bits = np.frombuffer(e["bits"] + b"\0" * 8, np.uint8).copy()
+    out = np.zeros(n, np.int16)
+    rc = fn(bits.ctypes.data_as(_vp), e["nbits"], len(e["rle"]), k, tv.ctypes.data_as(_vp),
+            tl.ctypes.data_as(_vp), tc.ctypes.data_as(_vp), n, out.ctypes.data_as(_vp))
+    assert rc == 0
+    return out.tolist()
+
+
+def ref_entropy(zz):
+    """The reference's own entropy stage on one stream (oracle/_ref), or None."""
+    L = ref_jpeg()
+    if L is None:
+        return None
+    fn = L.ref_jpeg_entropy
+    fn.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    return _entropy_call(fn, zz, True)
