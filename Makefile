@@ -18,7 +18,8 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -ffp-contract=off -fPIC -std=c++17 -Wall 
 CFLAGS_HOST := -O2 -fPIC -Wall -std=gnu11 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
 LIB     := $(PKG)/lz4jpeg/liblz4jpeg.so
 HDRS    := include/lz4r.h include/jpegr.h include/lz4jpeg_compat.h $(CSRC)/jpeg_tables.h
-OBJS    := $(B)/lz4r.o $(B)/lz4r_gpudec.o $(B)/jpegr.o $(B)/jpegr_blocks.o $(B)/synth.o \
+OBJS    := $(B)/lz4r.o $(B)/lz4r_gpudec.o $(B)/jpegr.o $(B)/jpegr_blocks.o $(B)/jpegr_entropy.o \
+           $(B)/synth.o \
            $(B)/lz4r_decode.o $(B)/compat.o
 
 all: lib bin oracle

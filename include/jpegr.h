@@ -101,6 +101,38 @@ int jpegr_permute_device(const void *d_in_f64, void *d_out_f64, const void *d_pe
 
 const char *jpegr_strerror(int code);
 
+/* Entropy stage (JPEG.c:767-1097, run by main at :1211-1349): per tile and
+ * channel -- Y 64, Cr 32, Cb 32 zigzagged ints in jpegr_encode_device's
+ * layout -- the RLE (count, value) ints (RLE, :767), the per-stream Huffman
+ * code exactly as encode_huffman builds it (first-occurrence frequencies
+ * :864, heap :895-936, tree :938 with its append-without-sift-up, DFS codes
+ * :964), and the encoded sequence (:993).  Output per tile (ntiles = all
+ * tiles of all images):
+ *   d_bits   256 B: [Y 128][Cr 64][Cb 64] bytes, bits packed MSB-first
+ *            (the reference's '0'/'1' chars)
+ *   d_meta   3 u32 (Y, Cr, Cb): nbits | rle_len << 16 | ncodes << 24
+ *   d_table  256 u32: [Y 128][Cr 64][Cb 64]; entry k = value (int16) |
+ *            code length << 16, in the reference's codes[] (DFS) order;
+ *            the codes follow from the lengths: code[0] = 0, code[k] =
+ *            (code[k-1] + 1) shifted left (or right) to length len[k]
+ * d_scratch: jpegr_entropy_scratch_bytes(ntiles) device bytes.  d_status:
+ * 2 u32 on the device; [0] = streams whose code or sequence would overflow
+ * the reference's char code[32] / sequence[1024|512] buffers (undefined
+ * behaviour there; truncated here).  Asynchronous on `stream`. */
+size_t jpegr_entropy_scratch_bytes(size_t ntiles);
+int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, void *d_bits,
+                                void *d_meta, void *d_table, void *d_scratch,
+                                void *d_status, void *stream);
+
+/* Inverse: bits + table -> RLE ints (decode_huffman, :1009; a one-code
+ * stream has an empty sequence and stands for rle_len copies of its symbol,
+ * which the reference keeps in its RLE array) -> ints (inverse_RLE, :810:
+ * counts clamped to the stream length, zero fill), written in
+ * jpegr_encode_device's layout.  d_status[1] = malformed streams. */
+int jpegr_entropy_decode_device(const void *d_bits, const void *d_meta,
+                                const void *d_table, size_t ntiles, void *d_coef,
+                                void *d_status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,464 @@
+// jpegr_entropy.hip -- the reference's JPEG entropy stage on MI355X:
+// per tile and channel, RLE of the zigzagged ints and a per-stream Huffman
+// code built exactly as the reference builds it, then the encoded bits; and
+// the inverse (decode + inverse RLE).  Algorithms/sequential/JPEG/JPEG.c:
+//   RLE                        :767-808   (count, value) ints
+//   calculate_frequency        :864-886   symbols in first-occurrence order
+//   heapify / build_heap       :895-936   min-heap on count (strict <, left first)
+//   build_huffman_tree         :938-962   pop, pop, APPEND the merged node and
+//                                          heapify its leaf index (a no-op: the
+//                                          node is not sifted up)
+//   assign_codes               :964-983   DFS, left '0' / right '1'
+//   generate_encoded_sequence  :993-1007
+//   decode_huffman             :1009-1033; inverse_RLE :810-840
+// The reference keeps codes as char strings and the sequence as '0'/'1'
+// chars; here the bits are packed MSB-first and the code table is the list of
+// (value, code length) in the reference's codes[] (DFS) order -- leaves of a
+// full binary tree listed left to right, so the codes follow from the lengths
+// (code[k] = (code[k-1] + 1) shifted to len[k]; left-aligned they increase).
+//
+// Mapping: one LANE per stream (a stream's work is a few hundred serial
+// steps; a wave per stream would issue each serial step for 64 lanes).  A
+// workgroup is one wave holding 64 tiles' streams of ONE channel, so Y
+// (64 ints, ~100 RLE symbols) and chroma (32 ints) never share a wave.  The
+// per-lane working set (symbols, counts, heap, tree, codes) lives in LDS
+// laid out column-per-lane, sized for <= 32 distinct symbols (random 4K
+// tiles: Y <= 21, chroma <= 10); a stream with more is deferred to a second
+// pass with the same code over global-memory scratch and room for 128.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/jpegr.h"
+
+namespace {
+
+constexpr int kLanes = 64;
+constexpr int kFastCap = 32;             // distinct symbols in the LDS pass
+constexpr int kFullCap = 128;            // RLE of 64 ints: <= 128 symbols
+constexpr int kPass2Lanes = 64 * 64;     // lanes of the deferred pass
+
+// per-tile output layout
+constexpr int kBitsPerTile = 256;        // bytes: [Y 128][Cr 64][Cb 64]
+constexpr int kTablePerTile = 256;       // u32 entries: [Y 128][Cr 64][Cb 64]
+
+__device__ __forceinline__ int stream_len(int c) { return c == 0 ? 64 : 32; }
+__device__ __forceinline__ int coef_off(int c) { return c == 0 ? 0 : c == 1 ? 64 : 96; }
+__device__ __forceinline__ int bits_off(int c) { return c == 0 ? 0 : c == 1 ? 128 : 192; }
+__device__ __forceinline__ int bits_cap(int c) { return c == 0 ? 1024 : 512; }
+// the reference's sequence buffers hold 1023 / 511 chars + NUL (JPEG.c:1248, :1286)
+__device__ __forceinline__ int ref_bits_max(int c) { return c == 0 ? 1023 : 511; }
+
+// Strided view of one lane's array: element i at p[i * stride].
+template <typename T>
+struct Col {
+  T *p;
+  int stride;
+  __device__ __forceinline__ T &operator[](int i) const { return p[i * stride]; }
+};
+
+// One lane's working set for a stream with at most Cap distinct symbols.
+struct Work {
+  Col<int16_t> sym;     // [Cap]       symbol values (the ints, without +1000)
+  Col<uint8_t> cnt;     // [2 Cap]     node counts (leaves, then merged nodes)
+  Col<uint8_t> uidx;    // [128]       leaf of each RLE position
+  Col<uint8_t> heap;    // [Cap]       node ids
+  Col<uint16_t> child;  // [Cap]       merged node -> left | right << 8
+  Col<uint32_t> code;   // [Cap]       leaf code bits (right-aligned)
+  Col<uint8_t> len;     // [Cap]       leaf code length
+  Col<uint16_t> stk;    // [Cap]       DFS stack: node | depth << 8
+};
+
+__device__ __forceinline__ void heapify(const Work &w, int size, int i) {   // JPEG.c:895
+  for (;;) {
+    int s = i;
+    const int l = 2 * i + 1, r = 2 * i + 2;
+    if (l < size && w.cnt[w.heap[l]] < w.cnt[w.heap[s]]) s = l;
+    if (r < size && w.cnt[w.heap[r]] < w.cnt[w.heap[s]]) s = r;
+    if (s == i) return;
+    const uint8_t t = w.heap[i];
+    w.heap[i] = w.heap[s];
+    w.heap[s] = t;
+    i = s;
+  }
+}
+
+enum : int { kOk = 0, kDefer = 1, kOverflow = 2 };
+
+// Encode one stream of n ints at zz (global).  Writes the packed bits (slot
+// of cap_bits), the table (value | len << 16 per code, DFS order) and the
+// meta word (nbits | rle_len << 16 | ncodes << 24).  Returns kOk, kDefer
+// (more than Cap distinct symbols; nothing written) or kOverflow (a code or
+// the sequence exceeds the reference's fixed buffers; written truncated).
+template <int Cap>
+__device__ int encode_stream(const int16_t *__restrict__ zz, int n, const Work &w,
+                             uint8_t *__restrict__ bits, int cap_bits, int ref_max,
+                             uint32_t *__restrict__ table, uint32_t *__restrict__ meta) {
+  // ---- RLE + frequencies in first-occurrence order (JPEG.c:767-808, :864-886)
+  int U = 0, R = 0;
+  bool defer = false;
+  auto emit = [&](int s) {
+    int u = 0;
+    while (u < U && w.sym[u] != s) ++u;
+    if (u == U) {
+      if (U == Cap) {
+        defer = true;
+        return;
+      }
+      w.sym[U] = (int16_t)s;
+      w.cnt[U] = 0;
+      ++U;
+    }
+    w.cnt[u] = (uint8_t)(w.cnt[u] + 1);
+    w.uidx[R++] = (uint8_t)u;
+  };
+  int cur = zz[0], run = 1;
+  for (int i = 1; i < n; ++i) {
+    const int v = zz[i];
+    if (v == cur) {
+      ++run;
+    } else {
+      emit(run);
+      emit(cur);
+      cur = v;
+      run = 1;
+    }
+  }
+  emit(run);
+  emit(cur);
+  if (defer) return kDefer;
+
+  // ---- heap and tree (JPEG.c:913-962) -------------------------------------
+  for (int i = 0; i < U; ++i) w.heap[i] = (uint8_t)i;
+  for (int i = U / 2 - 1; i >= 0; --i) heapify(w, U, i);
+  int size = U, next = U;
+  while (size > 1) {
+    const int left = w.heap[0];
+    w.heap[0] = w.heap[--size];
+    heapify(w, size, 0);
+    const int right = w.heap[0];
+    w.heap[0] = w.heap[--size];
+    heapify(w, size, 0);
+    w.cnt[next] = (uint8_t)(w.cnt[left] + w.cnt[right]);
+    w.child[next - U] = (uint16_t)(left | (right << 8));
+    w.heap[size++] = (uint8_t)next++;              // appended, not sifted up
+  }
+
+  // ---- codes: DFS, left first (JPEG.c:964-983) ------------------------------
+  // Leaves pop in codes[] order; each code follows from the previous one:
+  // code[k] = (code[k-1] + 1) moved to length len[k].
+  bool over = false;
+  int sp = 0, k = 0, plen = 0;
+  uint32_t pcode = 0;
+  w.stk[sp++] = (uint16_t)w.heap[0];                 // root, depth 0
+  while (sp) {
+    const int e = w.stk[--sp];
+    const int x = e & 255, d = e >> 8;
+    if (x < U) {                                      // leaf: next entry of codes[]
+      if (k) pcode = d >= plen ? (pcode + 1) << (d - plen) : (pcode + 1) >> (plen - d);
+      plen = d;
+      w.code[x] = pcode;
+      w.len[x] = (uint8_t)d;
+      if (d > 31) over = true;                        // char code[32] (JPEG.c:861)
+      table[k++] = (uint16_t)w.sym[x] | ((uint32_t)d << 16);
+      continue;
+    }
+    const int ch = w.child[x - U];
+    w.stk[sp++] = (uint16_t)((ch >> 8) | ((d + 1) << 8));      // right, visited second
+    w.stk[sp++] = (uint16_t)((ch & 255) | ((d + 1) << 8));     // left first
+  }
+
+  // ---- encoded sequence, MSB-first (JPEG.c:993-1007) ------------------------
+  uint64_t acc = 0;
+  int nacc = 0, nbits = 0, word = 0;
+  const int nwords = cap_bits / 32;
+  uint32_t *wout = reinterpret_cast<uint32_t *>(bits);
+  for (int j = 0; j < R; ++j) {
+    const int leaf = w.uidx[j];
+    const int L = w.len[leaf];
+    if (L > 32) break;                                // flagged above; no 64-bit overshift
+    acc = (acc << L) | w.code[leaf];
+    nacc += L;
+    nbits += L;
+    if (nacc >= 32) {
+      const uint32_t v = (uint32_t)(acc >> (nacc - 32));
+      if (word < nwords) wout[word] = __builtin_bswap32(v);
+      ++word;
+      nacc -= 32;
+    }
+  }
+  if (nacc && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc << (32 - nacc)));
+  if (nbits > ref_max) over = true;                   // char sequence[1024] / [512]
+  *meta = (uint32_t)(nbits < 0xFFFF ? nbits : 0xFFFF) | ((uint32_t)R << 16) |
+          ((uint32_t)U << 24);
+  return over ? kOverflow : kOk;
+}
+
+struct FastLds {
+  int16_t sym[kFastCap][kLanes];
+  uint8_t cnt[2 * kFastCap][kLanes];
+  uint8_t uidx[kFullCap][kLanes];
+  uint8_t heap[kFastCap][kLanes];
+  uint16_t child[kFastCap][kLanes];
+  uint32_t code[kFastCap][kLanes];
+  uint8_t len[kFastCap][kLanes];
+  uint16_t stk[kFastCap + 1][kLanes];
+};
+
+// scratch header (in d_scratch): [0] deferred count, then the deferred list
+struct ScratchHdr {
+  uint32_t ndefer;
+  uint32_t pad[3];
+};
+
+__global__ __launch_bounds__(kLanes) void entropy_encode_fast(
+    const int16_t *__restrict__ coef, size_t ntiles, uint8_t *__restrict__ bits,
+    uint32_t *__restrict__ meta, uint32_t *__restrict__ table, ScratchHdr *__restrict__ hdr,
+    uint32_t *__restrict__ deferred, uint32_t *__restrict__ status) {
+  __shared__ FastLds S;
+  const int lane = threadIdx.x;
+  const int c = (int)(blockIdx.x % 3);                      // channel of this wave
+  const size_t tile = (size_t)(blockIdx.x / 3) * kLanes + lane;
+  if (tile >= ntiles) return;
+  const Work w{{&S.sym[0][lane], kLanes}, {&S.cnt[0][lane], kLanes},
+               {&S.uidx[0][lane], kLanes}, {&S.heap[0][lane], kLanes},
+               {&S.child[0][lane], kLanes}, {&S.code[0][lane], kLanes},
+               {&S.len[0][lane], kLanes}, {&S.stk[0][lane], kLanes}};
+  const int rc = encode_stream<kFastCap>(
+      coef + tile * 128 + coef_off(c), stream_len(c), w, bits + tile * kBitsPerTile + bits_off(c),
+      bits_cap(c), ref_bits_max(c), table + tile * kTablePerTile + bits_off(c),
+      meta + tile * 3 + c);
+  if (rc == kDefer) {
+    const uint32_t slot = atomicAdd(&hdr->ndefer, 1u);
+    deferred[slot] = (uint32_t)(tile * 3 + c);
+  } else if (rc == kOverflow) {
+    atomicAdd(&status[0], 1u);
+  }
+}
+
+__global__ __launch_bounds__(kLanes) void entropy_encode_deferred(
+    const int16_t *__restrict__ coef, uint8_t *__restrict__ bits, uint32_t *__restrict__ meta,
+    uint32_t *__restrict__ table, const ScratchHdr *__restrict__ hdr,
+    const uint32_t *__restrict__ deferred, uint8_t *__restrict__ work,
+    uint32_t *__restrict__ status) {
+  const int gl = blockIdx.x * kLanes + threadIdx.x;          // this lane's scratch column
+  constexpr int NL = kPass2Lanes;
+  // column-per-lane arrays in global scratch (element i of lane gl at i*NL + gl)
+  int16_t *sym = reinterpret_cast<int16_t *>(work);                     // [Cap] i16
+  uint8_t *cnt = work + (size_t)NL * 2 * kFullCap;                      // [2 Cap]
+  uint8_t *uidx = cnt + (size_t)NL * 2 * kFullCap;                      // [128]
+  uint8_t *heap = uidx + (size_t)NL * kFullCap;                         // [Cap]
+  uint16_t *child = reinterpret_cast<uint16_t *>(heap + (size_t)NL * kFullCap);   // [Cap]
+  uint32_t *code = reinterpret_cast<uint32_t *>(child + (size_t)NL * kFullCap);   // [Cap]
+  uint8_t *len = reinterpret_cast<uint8_t *>(code + (size_t)NL * kFullCap);       // [Cap]
+  uint16_t *stk = reinterpret_cast<uint16_t *>(len + (size_t)NL * kFullCap);      // [Cap + 1]
+  const Work w{{sym + gl, NL}, {cnt + gl, NL}, {uidx + gl, NL}, {heap + gl, NL},
+               {child + gl, NL}, {code + gl, NL}, {len + gl, NL}, {stk + gl, NL}};
+  const uint32_t nd = hdr->ndefer;
+  for (uint32_t i = gl; i < nd; i += NL) {
+    const uint32_t s = deferred[i];
+    const size_t tile = s / 3;
+    const int c = (int)(s % 3);
+    const int rc = encode_stream<kFullCap>(
+        coef + tile * 128 + coef_off(c), stream_len(c), w,
+        bits + tile * kBitsPerTile + bits_off(c), bits_cap(c), ref_bits_max(c),
+        table + tile * kTablePerTile + bits_off(c), meta + tile * 3 + c);
+    if (rc != kOk) atomicAdd(&status[0], 1u);
+  }
+}
+
+// bytes of the deferred pass's per-lane working set
+constexpr size_t kWorkBytesPerLane = 2 * kFullCap /*sym*/ + 2 * kFullCap /*cnt*/ +
+                                     kFullCap /*uidx*/ + kFullCap /*heap*/ +
+                                     2 * kFullCap /*child*/ + 4 * kFullCap /*code*/ +
+                                     kFullCap /*len*/ + 2 * (kFullCap + 1) /*stk*/;
+
+// ---- decode ------------------------------------------------------------------
+
+constexpr int kDecCap = 64;                // codes held in LDS (more: read from global)
+
+struct DecLds {
+  uint32_t lc[kDecCap][kLanes];            // left-aligned codes, increasing
+  uint32_t vl[kDecCap][kLanes];            // value | len << 16
+};
+
+// Decode one stream: bits + table -> RLE ints (decode_huffman) -> n ints
+// (inverse_RLE: counts clamped to n, zero fill).  With one code (empty bit
+// string) the reference decodes nothing and keeps its RLE ints: rle_len
+// copies of the symbol.  Returns false on a malformed stream.
+template <typename LcT, typename VlT>
+__device__ bool decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
+                              const uint32_t *__restrict__ table, LcT lc, VlT vl,
+                              int16_t *__restrict__ out, int n) {
+  const int nbits = (int)(m & 0xFFFF), R = (int)((m >> 16) & 255), U = (int)(m >> 24);
+  if (U == 0 || R == 0 || R > 2 * n) return false;
+  // codes from the lengths, left to right (DFS order)
+  uint32_t code = 0;
+  int plen = 0;
+  for (int k = 0; k < U; ++k) {
+    const uint32_t e = table[k];
+    const int L = (int)((e >> 16) & 255);
+    if (L > 32 || (U > 1 && L == 0)) return false;
+    if (k) code = L >= plen ? (code + 1) << (L - plen) : (code + 1) >> (plen - L);
+    plen = L;
+    lc[k] = L ? code << (32 - L) : 0;
+    vl[k] = e;
+  }
+  int idx = 0, pending = -1;                        // pending: a count awaiting its value
+  auto put = [&](int v) {
+    if (pending < 0) {
+      pending = v;
+      return;
+    }
+    int cnt = pending;
+    pending = -1;
+    if (idx + cnt > n) cnt = n - idx;
+    for (int j = 0; j < cnt; ++j) out[idx++] = (int16_t)v;
+  };
+  if (U == 1) {
+    const int v = (int16_t)(vl[0] & 0xFFFF);
+    for (int j = 0; j < R; ++j) put(v);
+  } else {
+    const uint32_t *wds = reinterpret_cast<const uint32_t *>(bits);
+    int p = 0, got = 0;
+    while (p < nbits) {
+      // 32 bits at p (zero past the end)
+      const int wi = p >> 5, sh = p & 31;
+      const uint32_t w0 = __builtin_bswap32(wds[wi]);
+      const uint32_t w1 = (wi + 1) * 32 < nbits ? __builtin_bswap32(wds[wi + 1]) : 0;
+      uint32_t win = sh ? (w0 << sh) | (w1 >> (32 - sh)) : w0;
+      if (nbits - p < 32) win &= ~0u << (32 - (nbits - p));
+      // largest k with lc[k] <= win
+      int lo = 0, hi = U - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (lc[mid] <= win) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint32_t e = vl[lo];
+      const int L = (int)((e >> 16) & 255);
+      if (p + L > nbits) return false;
+      put((int16_t)(e & 0xFFFF));
+      p += L;
+      ++got;
+    }
+    if (got != R) return false;
+  }
+  while (idx < n) out[idx++] = 0;
+  return true;
+}
+
+// Streams with more codes than the LDS table holds (> 64: only luma streams
+// of nearly all-distinct ints): the codes are regenerated from the table for
+// every symbol and searched linearly -- slow, rare, no storage.
+__device__ bool decode_stream_slow(const uint8_t *__restrict__ bits, uint32_t m,
+                                   const uint32_t *__restrict__ table, int16_t *__restrict__ out,
+                                   int n) {
+  const int nbits = (int)(m & 0xFFFF), R = (int)((m >> 16) & 255), U = (int)(m >> 24);
+  if (R == 0 || R > 2 * n) return false;
+  const uint32_t *wds = reinterpret_cast<const uint32_t *>(bits);
+  int p = 0, got = 0, idx = 0, pending = -1;
+  while (p < nbits) {
+    const int wi = p >> 5, sh = p & 31;
+    const uint32_t w0 = __builtin_bswap32(wds[wi]);
+    const uint32_t w1 = (wi + 1) * 32 < nbits ? __builtin_bswap32(wds[wi + 1]) : 0;
+    uint32_t win = sh ? (w0 << sh) | (w1 >> (32 - sh)) : w0;
+    if (nbits - p < 32) win &= ~0u << (32 - (nbits - p));
+    uint32_t code = 0;
+    int plen = 0, hit = -1, L = 0;
+    for (int k = 0; k < U && hit < 0; ++k) {
+      L = (int)((table[k] >> 16) & 255);
+      if (L == 0 || L > 32) return false;
+      if (k) code = L >= plen ? (code + 1) << (L - plen) : (code + 1) >> (plen - L);
+      plen = L;
+      if ((win >> (32 - L)) == code) hit = k;
+    }
+    if (hit < 0 || p + L > nbits) return false;
+    const int v = (int16_t)(table[hit] & 0xFFFF);
+    if (pending < 0) {
+      pending = v;
+    } else {
+      int cnt = pending;
+      pending = -1;
+      if (idx + cnt > n) cnt = n - idx;
+      for (int j = 0; j < cnt; ++j) out[idx++] = (int16_t)v;
+    }
+    p += L;
+    ++got;
+  }
+  if (got != R) return false;
+  while (idx < n) out[idx++] = 0;
+  return true;
+}
+
+__global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
+    const uint8_t *__restrict__ bits, const uint32_t *__restrict__ meta,
+    const uint32_t *__restrict__ table, size_t ntiles, int16_t *__restrict__ coef,
+    uint32_t *__restrict__ status) {
+  __shared__ DecLds S;
+  const int lane = threadIdx.x;
+  const int c = (int)(blockIdx.x % 3);
+  const size_t tile = (size_t)(blockIdx.x / 3) * kLanes + lane;
+  if (tile >= ntiles) return;
+  const uint32_t m = meta[tile * 3 + c];
+  const int U = (int)(m >> 24);
+  const uint8_t *b = bits + tile * kBitsPerTile + bits_off(c);
+  const uint32_t *t = table + tile * kTablePerTile + bits_off(c);
+  int16_t *o = coef + tile * 128 + coef_off(c);
+  const bool ok = U <= kDecCap
+                      ? decode_stream(b, m, t, Col<uint32_t>{&S.lc[0][lane], kLanes},
+                                      Col<uint32_t>{&S.vl[0][lane], kLanes}, o, stream_len(c))
+                      : decode_stream_slow(b, m, t, o, stream_len(c));
+  if (!ok) atomicAdd(&status[1], 1u);
+}
+
+__global__ void entropy_init(ScratchHdr *hdr, uint32_t *status) {
+  hdr->ndefer = 0;
+  status[0] = 0;
+}
+
+}  // namespace
+
+extern "C" size_t jpegr_entropy_scratch_bytes(size_t ntiles) {
+  return 256 + ntiles * 3 * sizeof(uint32_t) + (size_t)kPass2Lanes * kWorkBytesPerLane;
+}
+
+extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, void *d_bits,
+                                           void *d_meta, void *d_table, void *d_scratch,
+                                           void *d_status, void *stream) {
+  if (!d_coef || !d_bits || !d_meta || !d_table || !d_scratch || !d_status || ntiles == 0 ||
+      ntiles > ((size_t)1 << 32) / 3)
+    return JPEGR_ERR_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto *hdr = static_cast<ScratchHdr *>(d_scratch);
+  auto *deferred = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_scratch) + 256);
+  auto *work = reinterpret_cast<uint8_t *>(deferred + ntiles * 3);
+  auto *status = static_cast<uint32_t *>(d_status);
+  hipLaunchKernelGGL(entropy_init, dim3(1), dim3(1), 0, s, hdr, status);
+  const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
+  hipLaunchKernelGGL(entropy_encode_fast, dim3(groups * 3), dim3(kLanes), 0, s,
+                     static_cast<const int16_t *>(d_coef), ntiles, static_cast<uint8_t *>(d_bits),
+                     static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
+                     deferred, status);
+  hipLaunchKernelGGL(entropy_encode_deferred, dim3(kPass2Lanes / kLanes), dim3(kLanes), 0, s,
+                     static_cast<const int16_t *>(d_coef), static_cast<uint8_t *>(d_bits),
+                     static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
+                     deferred, work, status);
+  return hipGetLastError() == hipSuccess ? JPEGR_OK : JPEGR_ERR_HIP;
+}
+
+extern "C" int jpegr_entropy_decode_device(const void *d_bits, const void *d_meta,
+                                           const void *d_table, size_t ntiles, void *d_coef,
+                                           void *d_status, void *stream) {
+  if (!d_bits || !d_meta || !d_table || !d_coef || !d_status || ntiles == 0 ||
+      ntiles > ((size_t)1 << 32) / 3)
+    return JPEGR_ERR_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(static_cast<uint32_t *>(d_status) + 1, 0, sizeof(uint32_t), s) != hipSuccess)
+    return JPEGR_ERR_HIP;
+  const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
+  hipLaunchKernelGGL(entropy_decode_kernel, dim3(groups * 3), dim3(kLanes), 0, s,
+                     static_cast<const uint8_t *>(d_bits), static_cast<const uint32_t *>(d_meta),
+                     static_cast<const uint32_t *>(d_table), ntiles,
+                     static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
+  return hipGetLastError() == hipSuccess ? JPEGR_OK : JPEGR_ERR_HIP;
+}

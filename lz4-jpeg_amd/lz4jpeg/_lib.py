@@ -39,6 +39,9 @@ SIGNATURES = [
     ("jpegr_encode", _i, [_vp, _i, _i, _vp]),
     ("jpegr_time_device", _i, [_vp, _i, _i, _i, _vp, _i, _vp, ctypes.POINTER(ctypes.c_float)]),
     ("jpegr_reconstruct_device", _i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
+    ("jpegr_entropy_scratch_bytes", _c_size, [_c_size]),
+    ("jpegr_entropy_encode_device", _i, [_vp, _c_size, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("jpegr_entropy_decode_device", _i, [_vp, _vp, _vp, _c_size, _vp, _vp, _vp]),
     ("jpegr_planes_device", _i, [_vp, _i, _i, _vp, _vp, _vp, _vp]),
     ("jpegr_dct_blocks_device", _i, [_vp, _i, _i, _i, _vp, _vp]),
     ("jpegr_quantize_device", _i, [_vp, _vp, _i, _c_size, _vp]),

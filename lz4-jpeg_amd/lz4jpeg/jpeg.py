@@ -91,3 +91,50 @@ def reconstruct_device(d_coef, w, h, nimg=1, d_orig=None, stream=None):
     if rc != 0:
         raise JpegError(rc, "jpegr_reconstruct_device")
     return out
+
+
+class Entropy:
+    """Device buffers of the entropy stage for `ntiles` tiles (all images):
+    bits (256 B/tile), meta (3 u32/tile), table (256 u32/tile), scratch and
+    the 2-word status (see jpegr.h)."""
+
+    def __init__(self, ntiles, device="cuda"):
+        import torch
+        self.ntiles = ntiles
+        self.bits = torch.zeros(ntiles * 256, dtype=torch.uint8, device=device)
+        self.meta = torch.zeros(ntiles * 3, dtype=torch.int32, device=device)
+        self.table = torch.zeros(ntiles * 256, dtype=torch.int32, device=device)
+        nscr = _lib.lib().jpegr_entropy_scratch_bytes(ntiles)
+        self.scratch = torch.empty(nscr, dtype=torch.uint8, device=device)
+        self.status = torch.zeros(2, dtype=torch.int32, device=device)
+
+    def encode(self, d_coef, stream=None):
+        """RLE + per-stream Huffman + encoded bits of every stream
+        (JPEG.c:767-1097) from encode_device's coefficients."""
+        rc = _lib.lib().jpegr_entropy_encode_device(
+            ctypes.c_void_p(d_coef.data_ptr()), self.ntiles, ctypes.c_void_p(self.bits.data_ptr()),
+            ctypes.c_void_p(self.meta.data_ptr()), ctypes.c_void_p(self.table.data_ptr()),
+            ctypes.c_void_p(self.scratch.data_ptr()), ctypes.c_void_p(self.status.data_ptr()),
+            _stream_handle(stream))
+        if rc != 0:
+            raise JpegError(rc, "jpegr_entropy_encode_device")
+
+    def decode(self, d_coef_out, stream=None):
+        """bits + tables -> coefficients (decode_huffman + inverse_RLE)."""
+        rc = _lib.lib().jpegr_entropy_decode_device(
+            ctypes.c_void_p(self.bits.data_ptr()), ctypes.c_void_p(self.meta.data_ptr()),
+            ctypes.c_void_p(self.table.data_ptr()), self.ntiles,
+            ctypes.c_void_p(d_coef_out.data_ptr()), ctypes.c_void_p(self.status.data_ptr()),
+            _stream_handle(stream))
+        if rc != 0:
+            raise JpegError(rc, "jpegr_entropy_decode_device")
+
+    def stream(self, tile, c):
+        """Host view of one stream: dict(rle_len, table [(value, len)], nbits, bits)."""
+        m = int(self.meta[tile * 3 + c].item()) & 0xFFFFFFFF
+        nbits, rle_len, ncodes = m & 0xFFFF, (m >> 16) & 255, m >> 24
+        off = (0, 128, 192)[c]
+        tab = self.table[tile * 256 + off: tile * 256 + off + ncodes].cpu().numpy()
+        table = [(int((e & 0xFFFF) ^ 0x8000) - 0x8000, int((e >> 16) & 255)) for e in tab.tolist()]
+        raw = self.bits[tile * 256 + off: tile * 256 + off + (nbits + 7) // 8].cpu().numpy()
+        return {"rle_len": rle_len, "table": table, "nbits": nbits, "bits": raw.tobytes()}

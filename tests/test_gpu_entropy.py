@@ -1,0 +1,134 @@
+"""GPU entropy stage (jpegr_entropy_encode_device / _decode_device, SURVEY.md
+§8 f2) against the reference: the committed known answers made by the
+reference's own RLE / encode_huffman / generate_encoded_sequence
+(tests/golden/entropy.json), the pinned oracle on whole images, and the
+decode round trip (the reference's decode_huffman + inverse_RLE is the
+identity on every stream).  All calls go through the C ABI."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import golden_inputs
+import oracle_api
+
+pytestmark = pytest.mark.gpu
+
+VECS = json.load(open(os.path.join(golden_inputs.GOLDEN, "entropy.json")))
+
+
+def _codes_from_lengths(lens):
+    out, code, plen = [], 0, 0
+    for k, L in enumerate(lens):
+        if k:
+            code = (code + 1) << (L - plen) if L >= plen else (code + 1) >> (plen - L)
+        plen = L
+        out.append(code)
+    return out
+
+
+def _pack(vecs):
+    """Tiles whose streams are the given vectors (64-int ones in Y slots,
+    32-int ones in Cr, then Cb); returns (coef int16 array, placement)."""
+    ys = [v for v in vecs if len(v["zz"]) == 64]
+    cs = [v for v in vecs if len(v["zz"]) == 32]
+    ntiles = max(len(ys), (len(cs) + 1) // 2)
+    coef = np.zeros((ntiles, 128), np.int16)
+    place = []
+    for t, v in enumerate(ys):
+        coef[t, :64] = v["zz"]
+        place.append((v, t, 0))
+    for i, v in enumerate(cs):
+        t, c = i // 2, 1 + i % 2
+        coef[t, 64 + 32 * (c - 1): 96 + 32 * (c - 1)] = v["zz"]
+        place.append((v, t, c))
+    return coef, place
+
+
+def test_golden_vectors(gpu):
+    import torch
+    from lz4jpeg import jpeg
+    coef, place = _pack(VECS)
+    d_coef = torch.from_numpy(coef.reshape(-1)).cuda()
+    ent = jpeg.Entropy(coef.shape[0])
+    ent.encode(d_coef)
+    torch.cuda.synchronize()
+    assert int(ent.status[0].item()) == 0
+    for v, t, c in place:
+        got = ent.stream(t, c)
+        assert got["rle_len"] == v["rle_len"], v["name"]
+        want = [(val, ln) for val, ln, _ in v["table"]]
+        assert got["table"] == want, v["name"]
+        assert _codes_from_lengths([ln for _, ln in want]) == [int(x) for _, _, x in v["table"]]
+        assert got["nbits"] == v["nbits"], v["name"]
+        assert got["bits"].hex() == v["bits"], v["name"]
+    out = torch.full_like(d_coef, 12345)
+    ent.decode(out)
+    torch.cuda.synchronize()
+    assert int(ent.status[1].item()) == 0
+    assert torch.equal(out, d_coef)
+
+
+def test_deferred_and_slow_paths(gpu, oracle):
+    """> 32 distinct symbols (second pass over global scratch) and > 64 codes
+    (decode without the LDS table), against the oracle."""
+    import torch
+    from lz4jpeg import jpeg
+    streams = [list(range(100, 164)), list(range(-40, 24)), [(-1) ** i * (i % 37) for i in range(64)],
+               list(range(0, 64, 2)) * 2]
+    coef = np.zeros((len(streams), 128), np.int16)
+    for t, zz in enumerate(streams):
+        coef[t, :64] = zz
+        coef[t, 64:96] = np.arange(32) - 16
+        coef[t, 96:] = np.arange(32) * 3
+    d_coef = torch.from_numpy(coef.reshape(-1)).cuda()
+    ent = jpeg.Entropy(coef.shape[0])
+    ent.encode(d_coef)
+    torch.cuda.synchronize()
+    assert int(ent.status[0].item()) == 0
+    for t in range(coef.shape[0]):
+        for c, sl in ((0, slice(0, 64)), (1, slice(64, 96)), (2, slice(96, 128))):
+            a = oracle_api.entropy(oracle, coef[t, sl])
+            got = ent.stream(t, c)
+            assert got["table"] == [(v, ln) for v, ln, _ in a["table"]], (t, c)
+            assert (got["nbits"], got["bits"]) == (a["nbits"], a["bits"]), (t, c)
+    out = torch.zeros_like(d_coef)
+    ent.decode(out)
+    torch.cuda.synchronize()
+    assert int(ent.status[1].item()) == 0
+    assert torch.equal(out, d_coef)
+
+
+@pytest.mark.parametrize("w,h,kind", [(3840, 2160, "rand"), (512, 384, "smooth"), (40, 24, "rand")])
+def test_image_vs_oracle_and_roundtrip(gpu, oracle, w, h, kind):
+    import torch
+    from lz4jpeg import jpeg
+    if kind == "rand":
+        img = oracle.rand_image(w, h, seed=1)
+    else:
+        yy, xx = np.mgrid[0:h, 0:w]
+        img = np.ascontiguousarray(np.stack([(xx // 3) % 256, (yy // 2) % 256,
+                                             ((xx + yy) // 5) % 256, np.full_like(xx, 255)],
+                                            -1).astype(np.uint8))
+    d_img = torch.from_numpy(img).cuda()
+    d_coef = jpeg.encode_device(d_img, w, h)
+    nt = jpeg.tiles(w, h)
+    ent = jpeg.Entropy(nt)
+    ent.encode(d_coef)
+    coef = d_coef.cpu().numpy().reshape(-1, 128)
+    torch.cuda.synchronize()
+    assert int(ent.status[0].item()) == 0
+    rng = np.random.default_rng(3)
+    for t in np.unique(np.concatenate([[0, nt - 1], rng.integers(0, nt, 200)])):
+        for c, sl in ((0, slice(0, 64)), (1, slice(64, 96)), (2, slice(96, 128))):
+            a = oracle_api.entropy(oracle, coef[t, sl])
+            got = ent.stream(int(t), c)
+            assert got["rle_len"] == len(a["rle"])
+            assert got["table"] == [(v, ln) for v, ln, _ in a["table"]], (t, c)
+            assert (got["nbits"], got["bits"]) == (a["nbits"], a["bits"]), (t, c)
+    out = torch.zeros_like(d_coef)
+    ent.decode(out)
+    torch.cuda.synchronize()
+    assert int(ent.status[1].item()) == 0
+    assert torch.equal(out, d_coef)
