@@ -21,8 +21,8 @@
 // steps; a wave per stream would issue each serial step for 64 lanes).  A
 // workgroup is one wave holding 64 tiles' streams of ONE channel, so Y
 // (64 ints, ~100 RLE symbols) and chroma (32 ints) never share a wave.  The
-// per-lane working set (symbols, counts, heap, tree, codes) lives in LDS
-// laid out column-per-lane, sized for <= 32 distinct symbols (random 4K
+// per-lane working set (symbol hash, heap with counts, tree, codes) lives
+// in LDS laid out dword-column-per-lane, sized for <= 32 distinct symbols (random 4K
 // tiles: Y <= 21, chroma <= 10); a stream with more is deferred to a second
 // pass with the same code over global-memory scratch and room for 128.
 #include <hip/hip_runtime.h>
@@ -56,91 +56,136 @@ struct Col {
   __device__ __forceinline__ T &operator[](int i) const { return p[i * stride]; }
 };
 
-// One lane's working set for a stream with at most Cap distinct symbols.
-struct Work {
-  Col<int16_t> sym;     // [Cap]       symbol values (the ints, without +1000)
-  Col<uint8_t> cnt;     // [2 Cap]     node counts (leaves, then merged nodes)
-  Col<uint8_t> uidx;    // [128]       leaf of each RLE position
-  Col<uint8_t> heap;    // [Cap]       node ids
-  Col<uint16_t> child;  // [Cap]       merged node -> left | right << 8
-  Col<uint32_t> code;   // [Cap]       leaf code bits (right-aligned)
-  Col<uint8_t> len;     // [Cap]       leaf code length
-  Col<uint16_t> stk;    // [Cap]       DFS stack: node | depth << 8
+// One lane's array in LDS, dword-column layout: the lane owns dword column
+// `lane` of a [rows][64] u32 block and packs 4 / sizeof(T) elements per
+// dword, so every lane hits its own bank whatever index it uses (a plain
+// [i][lane] byte column shares a dword between 4 lanes: up to 4-way
+// conflicts under divergent indices).
+template <typename T>
+struct LCol {
+  uint8_t *p;                                   // &block[0][lane] as bytes
+  __device__ __forceinline__ T &operator[](int i) const {
+    constexpr int per = 4 / (int)sizeof(T);
+    return *reinterpret_cast<T *>(p + (i / per) * (4 * kLanes) + (i % per) * (int)sizeof(T));
+  }
 };
 
-__device__ __forceinline__ void heapify(const Work &w, int size, int i) {   // JPEG.c:895
+// One lane's working set for a stream with at most Cap distinct symbols.
+template <template <typename> class A>
+struct Work {
+  A<int16_t> sym;       // [Cap]       leaf -> symbol value (the int, without +1000)
+  A<uint8_t> hash;      // [2 Cap]     open-addressing map symbol -> leaf + 1 (0 = empty)
+  A<uint16_t> heap;     // [Cap]       entries count << 8 | node id
+  A<uint16_t> child;    // [Cap]       merged node -> left | right << 8
+  A<uint32_t> code;     // [Cap]       leaf code bits (right-aligned)
+  A<uint8_t> len;       // [Cap]       leaf code length
+  A<uint16_t> stk;      // [Cap + 1]   DFS stack: node | depth << 8
+};
+
+// Sift the entry at i down (JPEG.c:895-911: smallest of i, left, right by
+// count with strict <, left tested first), holding it in registers and
+// moving children up into the hole -- the same final arrangement as the
+// reference's swaps.
+template <class W>
+__device__ __forceinline__ void heapify(const W &w, int size, int i) {
+  const uint16_t x = w.heap[i];
+  const int cx = x >> 8;
   for (;;) {
-    int s = i;
-    const int l = 2 * i + 1, r = 2 * i + 2;
-    if (l < size && w.cnt[w.heap[l]] < w.cnt[w.heap[s]]) s = l;
-    if (r < size && w.cnt[w.heap[r]] < w.cnt[w.heap[s]]) s = r;
-    if (s == i) return;
-    const uint8_t t = w.heap[i];
-    w.heap[i] = w.heap[s];
-    w.heap[s] = t;
+    const int l = 2 * i + 1, r = l + 1;
+    if (l >= size) break;
+    const uint16_t hl = w.heap[l];
+    const uint16_t hr = r < size ? w.heap[r] : (uint16_t)0xFFFF;
+    int s = i, cs = cx;
+    uint16_t hs = x;
+    if ((hl >> 8) < cs) { s = l; cs = hl >> 8; hs = hl; }
+    if (r < size && (hr >> 8) < cs) { s = r; hs = hr; }
+    if (s == i) break;
+    w.heap[i] = hs;
     i = s;
   }
+  w.heap[i] = x;
 }
 
 enum : int { kOk = 0, kDefer = 1, kOverflow = 2 };
+
+__device__ __forceinline__ int hash_slot(int s, int mask) {
+  return (int)(((uint32_t)(s + 1024) * 0x9E3779B1u) >> 24) & mask;
+}
 
 // Encode one stream of n ints at zz (global).  Writes the packed bits (slot
 // of cap_bits), the table (value | len << 16 per code, DFS order) and the
 // meta word (nbits | rle_len << 16 | ncodes << 24).  Returns kOk, kDefer
 // (more than Cap distinct symbols; nothing written) or kOverflow (a code or
 // the sequence exceeds the reference's fixed buffers; written truncated).
-template <int Cap>
-__device__ int encode_stream(const int16_t *__restrict__ zz, int n, const Work &w,
+template <int Cap, class W>
+__device__ int encode_stream(const int16_t *__restrict__ zz, int n, const W &w,
                              uint8_t *__restrict__ bits, int cap_bits, int ref_max,
                              uint32_t *__restrict__ table, uint32_t *__restrict__ meta) {
-  // ---- RLE + frequencies in first-occurrence order (JPEG.c:767-808, :864-886)
-  int U = 0, R = 0;
-  bool defer = false;
-  auto emit = [&](int s) {
-    int u = 0;
-    while (u < U && w.sym[u] != s) ++u;
-    if (u == U) {
-      if (U == Cap) {
-        defer = true;
-        return;
+  constexpr int kMask = 2 * Cap - 1;
+  // symbol -> leaf through the hash (inserting new symbols in first-occurrence
+  // order, JPEG.c:864-886); returns -1 when a new symbol does not fit
+  int U = 0;
+  auto leaf_of = [&](int s, bool insert) -> int {
+    int h = hash_slot(s, kMask);
+    for (;;) {
+      const int e = w.hash[h];
+      if (e == 0) {
+        if (!insert || U == Cap) return -1;
+        w.hash[h] = (uint8_t)(U + 1);
+        w.sym[U] = (int16_t)s;
+        w.heap[U] = (uint16_t)U;                    // count 0, id U
+        return U++;
       }
-      w.sym[U] = (int16_t)s;
-      w.cnt[U] = 0;
-      ++U;
+      if (w.sym[e - 1] == s) return e - 1;
+      h = (h + 1) & kMask;
     }
-    w.cnt[u] = (uint8_t)(w.cnt[u] + 1);
-    w.uidx[R++] = (uint8_t)u;
   };
-  int cur = zz[0], run = 1;
-  for (int i = 1; i < n; ++i) {
-    const int v = zz[i];
-    if (v == cur) {
-      ++run;
-    } else {
-      emit(run);
-      emit(cur);
-      cur = v;
-      run = 1;
+  for (int i = 0; i <= kMask; ++i) w.hash[i] = 0;
+
+  // ---- RLE (JPEG.c:767-808) + frequencies --------------------------------------
+  int R = 0;
+  bool defer = false;
+  auto count = [&](int s) {
+    const int u = leaf_of(s, true);
+    if (u < 0) {
+      defer = true;
+      return;
+    }
+    w.heap[u] = (uint16_t)(w.heap[u] + 256);
+    ++R;
+  };
+  {
+    int cur = zz[0], run = 1;
+    for (int i = 1; i < n && !defer; ++i) {
+      const int v = zz[i];
+      if (v == cur) {
+        ++run;
+      } else {
+        count(run);
+        count(cur);
+        cur = v;
+        run = 1;
+      }
+    }
+    if (!defer) {
+      count(run);
+      count(cur);
     }
   }
-  emit(run);
-  emit(cur);
   if (defer) return kDefer;
 
   // ---- heap and tree (JPEG.c:913-962) -------------------------------------
-  for (int i = 0; i < U; ++i) w.heap[i] = (uint8_t)i;
   for (int i = U / 2 - 1; i >= 0; --i) heapify(w, U, i);
   int size = U, next = U;
   while (size > 1) {
-    const int left = w.heap[0];
+    const uint16_t left = w.heap[0];
     w.heap[0] = w.heap[--size];
     heapify(w, size, 0);
-    const int right = w.heap[0];
+    const uint16_t right = w.heap[0];
     w.heap[0] = w.heap[--size];
     heapify(w, size, 0);
-    w.cnt[next] = (uint8_t)(w.cnt[left] + w.cnt[right]);
-    w.child[next - U] = (uint16_t)(left | (right << 8));
-    w.heap[size++] = (uint8_t)next++;              // appended, not sifted up
+    w.child[next - U] = (uint16_t)((left & 255) | ((right & 255) << 8));
+    w.heap[size++] = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next++);   // not sifted up
   }
 
   // ---- codes: DFS, left first (JPEG.c:964-983) ------------------------------
@@ -149,7 +194,7 @@ __device__ int encode_stream(const int16_t *__restrict__ zz, int n, const Work &
   bool over = false;
   int sp = 0, k = 0, plen = 0;
   uint32_t pcode = 0;
-  w.stk[sp++] = (uint16_t)w.heap[0];                 // root, depth 0
+  w.stk[sp++] = (uint16_t)(w.heap[0] & 255);         // root, depth 0
   while (sp) {
     const int e = w.stk[--sp];
     const int x = e & 255, d = e >> 8;
@@ -167,15 +212,15 @@ __device__ int encode_stream(const int16_t *__restrict__ zz, int n, const Work &
     w.stk[sp++] = (uint16_t)((ch & 255) | ((d + 1) << 8));     // left first
   }
 
-  // ---- encoded sequence, MSB-first (JPEG.c:993-1007) ------------------------
+  // ---- encoded sequence, MSB-first (JPEG.c:993-1007): RLE again --------------
   uint64_t acc = 0;
   int nacc = 0, nbits = 0, word = 0;
   const int nwords = cap_bits / 32;
   uint32_t *wout = reinterpret_cast<uint32_t *>(bits);
-  for (int j = 0; j < R; ++j) {
-    const int leaf = w.uidx[j];
+  auto put = [&](int s) {
+    const int leaf = leaf_of(s, false);
     const int L = w.len[leaf];
-    if (L > 32) break;                                // flagged above; no 64-bit overshift
+    if (L > 32) return;                               // flagged above; no 64-bit overshift
     acc = (acc << L) | w.code[leaf];
     nacc += L;
     nbits += L;
@@ -185,6 +230,22 @@ __device__ int encode_stream(const int16_t *__restrict__ zz, int n, const Work &
       ++word;
       nacc -= 32;
     }
+  };
+  {
+    int cur = zz[0], run = 1;
+    for (int i = 1; i < n; ++i) {
+      const int v = zz[i];
+      if (v == cur) {
+        ++run;
+      } else {
+        put(run);
+        put(cur);
+        cur = v;
+        run = 1;
+      }
+    }
+    put(run);
+    put(cur);
   }
   if (nacc && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc << (32 - nacc)));
   if (nbits > ref_max) over = true;                   // char sequence[1024] / [512]
@@ -193,15 +254,18 @@ __device__ int encode_stream(const int16_t *__restrict__ zz, int n, const Work &
   return over ? kOverflow : kOk;
 }
 
+template <typename T>
+using GColT = Col<T>;
+
+// dword-column blocks ([rows][64] u32), rows = elements * size / 4
 struct FastLds {
-  int16_t sym[kFastCap][kLanes];
-  uint8_t cnt[2 * kFastCap][kLanes];
-  uint8_t uidx[kFullCap][kLanes];
-  uint8_t heap[kFastCap][kLanes];
-  uint16_t child[kFastCap][kLanes];
+  uint32_t sym[kFastCap / 2][kLanes];
+  uint32_t hash[2 * kFastCap / 4][kLanes];
+  uint32_t heap[kFastCap / 2][kLanes];
+  uint32_t child[kFastCap / 2][kLanes];
   uint32_t code[kFastCap][kLanes];
-  uint8_t len[kFastCap][kLanes];
-  uint16_t stk[kFastCap + 1][kLanes];
+  uint32_t len[kFastCap / 4][kLanes];
+  uint32_t stk[(kFastCap + 2) / 2][kLanes];
 };
 
 // scratch header (in d_scratch): [0] deferred count, then the deferred list
@@ -219,10 +283,9 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_fast(
   const int c = (int)(blockIdx.x % 3);                      // channel of this wave
   const size_t tile = (size_t)(blockIdx.x / 3) * kLanes + lane;
   if (tile >= ntiles) return;
-  const Work w{{&S.sym[0][lane], kLanes}, {&S.cnt[0][lane], kLanes},
-               {&S.uidx[0][lane], kLanes}, {&S.heap[0][lane], kLanes},
-               {&S.child[0][lane], kLanes}, {&S.code[0][lane], kLanes},
-               {&S.len[0][lane], kLanes}, {&S.stk[0][lane], kLanes}};
+  auto col = [&](uint32_t(*blk)[kLanes]) { return reinterpret_cast<uint8_t *>(&blk[0][lane]); };
+  const Work<LCol> w{{col(S.sym)}, {col(S.hash)}, {col(S.heap)}, {col(S.child)},
+                     {col(S.code)}, {col(S.len)}, {col(S.stk)}};
   const int rc = encode_stream<kFastCap>(
       coef + tile * 128 + coef_off(c), stream_len(c), w, bits + tile * kBitsPerTile + bits_off(c),
       bits_cap(c), ref_bits_max(c), table + tile * kTablePerTile + bits_off(c),
@@ -243,16 +306,15 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_deferred(
   const int gl = blockIdx.x * kLanes + threadIdx.x;          // this lane's scratch column
   constexpr int NL = kPass2Lanes;
   // column-per-lane arrays in global scratch (element i of lane gl at i*NL + gl)
-  int16_t *sym = reinterpret_cast<int16_t *>(work);                     // [Cap] i16
-  uint8_t *cnt = work + (size_t)NL * 2 * kFullCap;                      // [2 Cap]
-  uint8_t *uidx = cnt + (size_t)NL * 2 * kFullCap;                      // [128]
-  uint8_t *heap = uidx + (size_t)NL * kFullCap;                         // [Cap]
-  uint16_t *child = reinterpret_cast<uint16_t *>(heap + (size_t)NL * kFullCap);   // [Cap]
-  uint32_t *code = reinterpret_cast<uint32_t *>(child + (size_t)NL * kFullCap);   // [Cap]
-  uint8_t *len = reinterpret_cast<uint8_t *>(code + (size_t)NL * kFullCap);       // [Cap]
-  uint16_t *stk = reinterpret_cast<uint16_t *>(len + (size_t)NL * kFullCap);      // [Cap + 1]
-  const Work w{{sym + gl, NL}, {cnt + gl, NL}, {uidx + gl, NL}, {heap + gl, NL},
-               {child + gl, NL}, {code + gl, NL}, {len + gl, NL}, {stk + gl, NL}};
+  int16_t *sym = reinterpret_cast<int16_t *>(work);                             // [Cap]
+  uint8_t *hash = work + (size_t)NL * 2 * kFullCap;                             // [2 Cap]
+  uint16_t *heap = reinterpret_cast<uint16_t *>(hash + (size_t)NL * 2 * kFullCap);   // [Cap]
+  uint16_t *child = heap + (size_t)NL * kFullCap;                               // [Cap]
+  uint32_t *code = reinterpret_cast<uint32_t *>(child + (size_t)NL * kFullCap); // [Cap]
+  uint8_t *len = reinterpret_cast<uint8_t *>(code + (size_t)NL * kFullCap);     // [Cap]
+  uint16_t *stk = reinterpret_cast<uint16_t *>(len + (size_t)NL * kFullCap);    // [Cap + 1]
+  const Work<GColT> w{{sym + gl, NL}, {hash + gl, NL}, {heap + gl, NL}, {child + gl, NL},
+                      {code + gl, NL}, {len + gl, NL}, {stk + gl, NL}};
   const uint32_t nd = hdr->ndefer;
   for (uint32_t i = gl; i < nd; i += NL) {
     const uint32_t s = deferred[i];
@@ -267,10 +329,10 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_deferred(
 }
 
 // bytes of the deferred pass's per-lane working set
-constexpr size_t kWorkBytesPerLane = 2 * kFullCap /*sym*/ + 2 * kFullCap /*cnt*/ +
-                                     kFullCap /*uidx*/ + kFullCap /*heap*/ +
-                                     2 * kFullCap /*child*/ + 4 * kFullCap /*code*/ +
-                                     kFullCap /*len*/ + 2 * (kFullCap + 1) /*stk*/;
+constexpr size_t kWorkBytesPerLane = 2 * kFullCap /*sym*/ + 2 * kFullCap /*hash*/ +
+                                     2 * kFullCap /*heap*/ + 2 * kFullCap /*child*/ +
+                                     4 * kFullCap /*code*/ + kFullCap /*len*/ +
+                                     2 * (kFullCap + 1) /*stk*/;
 
 // ---- decode ------------------------------------------------------------------
 
