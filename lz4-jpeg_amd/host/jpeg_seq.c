@@ -11,8 +11,11 @@
  *          coefficients: int16 LE per 8x8 tile [Y 64][Cr 32][Cb 32], tiles
  *          in raster order (the reference keeps them in memory only)
  *   exit 0; unreadable image: "Error loading image" and exit(1) (JPEG.c:74-78).
- * Colour planes, DCT, quantisation, zigzag and the reconstruction (reverse
- * zigzag, dequantisation, IDCT, YCbCr->RGB) run on the GPU (jpegr_*).
+ * Colour planes, DCT, quantisation, zigzag, the entropy round trip the
+ * reference runs per tile (RLE + Huffman encode, decode, inverse RLE,
+ * JPEG.c:1211-1349) and the reconstruction (reverse zigzag, dequantisation,
+ * IDCT, YCbCr->RGB) run on the GPU (jpegr_*); reconstructed.png is decoded
+ * from the entropy-decoded coefficients, as in the reference.
  * Optional argv[1] / argv[2] override the input image / output directory.
  */
 #include <stdint.h>
@@ -54,17 +57,32 @@ int main(int argc, char **argv) {
   }
   const size_t npx = (size_t)w * h;
   const size_t ncoef = jpegr_coef_count(w, h);
+  const size_t ntiles = ncoef / 128;
   void *d_rgba = NULL, *d_y = NULL, *d_cr = NULL, *d_cb = NULL, *d_coef = NULL, *d_rec = NULL;
+  void *d_bits = NULL, *d_meta = NULL, *d_table = NULL, *d_scr = NULL, *d_st = NULL;
+  void *d_coef2 = NULL;
   if (hipMalloc(&d_rgba, npx * 4) != hipSuccess || hipMalloc(&d_y, npx) != hipSuccess ||
       hipMalloc(&d_rec, npx * 4) != hipSuccess ||
       hipMalloc(&d_cr, npx) != hipSuccess || hipMalloc(&d_cb, npx) != hipSuccess ||
-      hipMalloc(&d_coef, ncoef * 2) != hipSuccess)
+      hipMalloc(&d_coef, ncoef * 2) != hipSuccess || hipMalloc(&d_coef2, ncoef * 2) != hipSuccess ||
+      hipMalloc(&d_bits, ntiles * 256) != hipSuccess ||
+      hipMalloc(&d_meta, ntiles * 3 * 4) != hipSuccess ||
+      hipMalloc(&d_table, ntiles * 256 * 4) != hipSuccess ||
+      hipMalloc(&d_scr, jpegr_entropy_scratch_bytes(ntiles)) != hipSuccess ||
+      hipMalloc(&d_st, 8) != hipSuccess)
     fail("device allocation failed");
   if (hipMemcpy(d_rgba, rgba, npx * 4, hipMemcpyHostToDevice) != hipSuccess) fail("copy in");
   if (jpegr_planes_device(d_rgba, w, h, d_y, d_cr, d_cb, NULL) != JPEGR_OK ||
       jpegr_encode_device(d_rgba, w, h, 1, d_coef, NULL) != JPEGR_OK ||
-      jpegr_reconstruct_device(d_coef, d_rgba, w, h, 1, d_rec, NULL) != JPEGR_OK)
+      jpegr_entropy_encode_device(d_coef, ntiles, d_bits, d_meta, d_table, d_scr, d_st, NULL) !=
+          JPEGR_OK ||
+      jpegr_entropy_decode_device(d_bits, d_meta, d_table, ntiles, d_coef2, d_st, NULL) !=
+          JPEGR_OK ||
+      jpegr_reconstruct_device(d_coef2, d_rgba, w, h, 1, d_rec, NULL) != JPEGR_OK)
     fail("kernel launch");
+  uint32_t st[2];
+  if (hipMemcpy(st, d_st, 8, hipMemcpyDeviceToHost) != hipSuccess) fail("copy out");
+  if (st[1] != 0) fail("entropy decode");
   uint8_t *y = malloc(npx), *cr = malloc(npx), *cb = malloc(npx), *vis = malloc(npx * 4);
   uint8_t *rec = malloc(npx * 4);
   int16_t *coef = malloc(ncoef * 2);
@@ -104,7 +122,8 @@ int main(int argc, char **argv) {
   if (!f || fwrite(coef, 2, ncoef, f) != ncoef) fail("cannot write coefficients.bin");
   fclose(f);
   (void)hipFree(d_rgba); (void)hipFree(d_y); (void)hipFree(d_cr); (void)hipFree(d_cb);
-  (void)hipFree(d_coef); (void)hipFree(d_rec);
+  (void)hipFree(d_coef); (void)hipFree(d_rec); (void)hipFree(d_coef2); (void)hipFree(d_bits);
+  (void)hipFree(d_meta); (void)hipFree(d_table); (void)hipFree(d_scr); (void)hipFree(d_st);
   free(rgba); free(y); free(cr); free(cb); free(vis); free(coef); free(rec);
   return 0;
 }
