@@ -1,4 +1,4 @@
-"""Diagnostic: per-phase s_memtime totals of the LZ4R_VARIANT=5 build."""
+"""Diagnostic: per-phase s_memtime totals of a LZ4R_PROF build (tools/build_variants.sh)."""
 import ctypes
 import os
 import sys
@@ -18,8 +18,8 @@ d_out = torch.empty(lz4.compress_bound(n), dtype=torch.uint8, device="cuda")
 _, got = c.compress_device(d_in, n, d_out)
 buf = (ctypes.c_ulonglong * 16)()
 _lib.lib().lz4r_debug_prof(buf)
-names = ["index+close", "walk", "drain", "scan+nm+succ", "parse", "seqs", "literals",
-         "stage/loop", "lookback", "store"]
+names = ["index (sort)", "candidates+lcp", "sync", "best+nm+succ", "walk+visit", "sequences",
+         "literals", "block start", "bsizes", "store"]
 tot = sum(buf[:10])
 for i, nm in enumerate(names):
     print(f"{nm:14s} {buf[i] / 1e9:8.3f} Gcyc  {100 * buf[i] / tot:5.1f}%")
