@@ -50,7 +50,8 @@
 #include "../../include/lz4r.h"
 
 // LZ4R_VARIANT (timing ablations only, never shipped): 1 = no match search,
-// 2 = no index/match phase, 6 = input from a 150 KB hot set (isolates the
+// 2 = no index/match phase, 3 = index only (no candidates), 4 = candidates
+// without the lcp verification, 6 = input from a 150 KB hot set (isolates the
 // HBM fetch: 7.27 vs 7.00 ms on 1 GiB -- the fetch is hidden by occupancy)
 #ifndef LZ4R_VARIANT
 #define LZ4R_VARIANT 0
@@ -287,7 +288,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
     int ncand = 0;
     auto drain = [&]() {
       __syncthreads();
-      for (int i = lane; i < ncand; i += 64) {
+      for (int i = lane; i < ncand && LZ4R_VARIANT != 4; i += 64) {
         const uint32_t pr = S.seq[i];
         const int p = (int)(pr & 0xFFFFu), j = (int)(pr >> 16);
         const int l = lcp(S.buf, base + j, base + p, n - p);
@@ -323,19 +324,39 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
       S.seq[sl] = (uint32_t)p | ((uint32_t)j << 16);
       ncand += __popcll(cm);
     };
+    // The round's pairs are spread evenly over the lanes: entry e (lane e of
+    // the round) owns pairs [o_e, o_e + len_e) of the round's pair space
+    // (exclusive scan); pair q = base + lane finds its owner through a head
+    // marker (LDS max) and a wave max-scan, then fetches the partner entry.
+    // A round costs ceil(pairs / 64) steps instead of max(len) / 2 (one
+    // large bucket kept most lanes idle: 1,223 lane-slots per text block for
+    // ~138 pairs).  The bucket words double as the 64 head markers here
+    // (bucket starts are already in registers; they are cleared after).
+    uint32_t *head = S.cnt;
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-      if (r * 64 >= nk) break;
+      if (r * 64 >= nk || LZ4R_VARIANT == 3) break;
       const uint32_t me = meR[r];
       const int beg = begR[r], len = lenR[r];
-      // two members per step: independent loads, one latency
-      for (int it = 0; __ballot(it < len); it += 2) {
-        const bool a0 = it < len, a1 = it + 1 < len;
-        const uint32_t o0 = a0 ? S.srt[beg + it] : 0u;
-        const uint32_t o1 = a1 ? S.srt[beg + it + 1] : 0u;
-        pair(me, o0, a0);
-        pair(me, o1, a1);
-        if (ncand > kTrash - 128) {
+      const uint32_t incl = wave_incl_add((uint32_t)len);
+      const int o = (int)incl - len;
+      const int Pr = (int)lane63(incl);
+      const uint32_t bo = (uint32_t)beg | ((uint32_t)o << 9);      // o < 2^16 (<= 297*296/2)
+      for (int base = 0; base < Pr; base += 64) {
+        head[lane] = 0u;
+        __syncthreads();
+        if (len > 0 && o < base + 64 && o + len > base)
+          atomicMax(&head[o > base ? o - base : 0], (uint32_t)lane + 1u);
+        __syncthreads();
+        const int owner = (int)wave_incl_max(head[lane]) - 1;
+        const int q = base + lane;
+        const bool act = q < Pr;
+        const uint32_t meL = (uint32_t)__shfl((int)me, owner, 64);
+        const uint32_t boL = (uint32_t)__shfl((int)bo, owner, 64);
+        const int k = (int)(boL & 511u) + (q - (int)(boL >> 9));
+        const uint32_t ok = act ? S.srt[k] : 0u;
+        pair(meL, ok, act);
+        if (ncand > kTrash - 64) {
           drain();
           ncand = 0;
         }
