@@ -116,16 +116,19 @@ __device__ __forceinline__ uint32_t load4u(const uint8_t *b, int off) {
   return __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(off & 3));
 }
 
+typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned 8-byte LDS access
+
 // Longest common prefix of the byte runs at a and b (a < b), capped at
 // `limit` = n - b: the canonical clamp (a match never crosses the block end).
-// 8 bytes per step.
+// 8 bytes per step as one unaligned ds_read_b64 per side (the LDS runs in
+// unaligned mode); reads past the region land in its pad.
 __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
   int l = 0;
   while (l < limit) {
-    const uint32_t x0 = load4u(d, a + l) ^ load4u(d, b + l);
-    const uint32_t x1 = load4u(d, a + l + 4) ^ load4u(d, b + l + 4);
-    if (x0 | x1) {
-      l += x0 ? (__builtin_ctz(x0) >> 3) : 4 + (__builtin_ctz(x1) >> 3);
+    const uint64_t x = *reinterpret_cast<const u64u *>(d + a + l) ^
+                       *reinterpret_cast<const u64u *>(d + b + l);
+    if (x) {
+      l += __builtin_ctzll(x) >> 3;
       return l < limit ? l : limit;
     }
     l += 8;
