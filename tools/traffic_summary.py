@@ -26,11 +26,17 @@ def per_launch(db, counter, kernel_sub):
 def main(d):
     out = {}
     for kern, run, sub in (("lz4", "lz4", "lz4_tiles"), ("lz4_gather", "lz4", "lz4_gather"),
-                           ("jpeg", "jpeg", "jpeg_strip_kernel")):
+                           ("jpeg", "jpeg", "jpeg_strip_kernel"),
+                           ("lz4_decode", "dec", "lz4_decode_blocks"),
+                           ("entropy_encode", "ent", "entropy_encode_fast"),
+                           ("entropy_decode", "ent", "entropy_decode_kernel")):
         f = per_launch(os.path.join(d, f"{run}_fetch", "run_results.db"), "FETCH_SIZE", sub)
         w = per_launch(os.path.join(d, f"{run}_write", "run_results.db"), "WRITE_SIZE", sub)
         if not f or not w:
             continue
+        # the x2 rule is stated for 16-B-per-lane streaming reads (lz4_tiles,
+        # jpeg); the decoder / entropy kernels read 2..16 B per lane, so their
+        # doubled figure is an upper estimate -- the raw KiB are kept beside it
         fetch = 2 * 1024 * sum(f) / len(f)
         write = 1024 * sum(w) / len(w)
         out[kern] = {"kernel": sub, "fetch_bytes": fetch, "write_bytes": write,
