@@ -341,6 +341,7 @@ constexpr int kDecCap = 64;                // codes held in LDS (more: read from
 struct DecLds {
   uint32_t lc[kDecCap][kLanes];            // left-aligned codes, increasing
   uint32_t vl[kDecCap][kLanes];            // value | len << 16
+  alignas(16) int16_t out[kLanes][64];     // the lane's decoded ints (leave as 16-B stores)
 };
 
 // Decode one stream: bits + table -> RLE ints (decode_huffman) -> n ints
@@ -465,12 +466,18 @@ __global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
   const int U = (int)(m >> 24);
   const uint8_t *b = bits + tile * kBitsPerTile + bits_off(c);
   const uint32_t *t = table + tile * kTablePerTile + bits_off(c);
-  int16_t *o = coef + tile * 128 + coef_off(c);
+  // ints are produced one at a time: collect them in LDS, then 16-B stores
+  // (2-byte stores to 64 scattered streams wrote ~6x the bytes)
+  int16_t *o = S.out[lane];
+  const int n = stream_len(c);
   const bool ok = U <= kDecCap
                       ? decode_stream(b, m, t, Col<uint32_t>{&S.lc[0][lane], kLanes},
-                                      Col<uint32_t>{&S.vl[0][lane], kLanes}, o, stream_len(c))
-                      : decode_stream_slow(b, m, t, o, stream_len(c));
+                                      Col<uint32_t>{&S.vl[0][lane], kLanes}, o, n)
+                      : decode_stream_slow(b, m, t, o, n);
   if (!ok) atomicAdd(&status[1], 1u);
+  uint4 *dst = reinterpret_cast<uint4 *>(coef + tile * 128 + coef_off(c));
+  const uint4 *src = reinterpret_cast<const uint4 *>(o);
+  for (int v = 0; v < n / 8; ++v) dst[v] = src[v];
 }
 
 __global__ void entropy_init(ScratchHdr *hdr, uint32_t *status) {
@@ -488,7 +495,8 @@ extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, vo
                                            void *d_meta, void *d_table, void *d_scratch,
                                            void *d_status, void *stream) {
   if (!d_coef || !d_bits || !d_meta || !d_table || !d_scratch || !d_status || ntiles == 0 ||
-      ntiles > ((size_t)1 << 32) / 3)
+      ntiles > ((size_t)1 << 32) / 3 || (reinterpret_cast<uintptr_t>(d_coef) & 15) != 0 ||
+      (reinterpret_cast<uintptr_t>(d_bits) & 3) != 0)
     return JPEGR_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   auto *hdr = static_cast<ScratchHdr *>(d_scratch);
@@ -512,7 +520,8 @@ extern "C" int jpegr_entropy_decode_device(const void *d_bits, const void *d_met
                                            const void *d_table, size_t ntiles, void *d_coef,
                                            void *d_status, void *stream) {
   if (!d_bits || !d_meta || !d_table || !d_coef || !d_status || ntiles == 0 ||
-      ntiles > ((size_t)1 << 32) / 3)
+      ntiles > ((size_t)1 << 32) / 3 || (reinterpret_cast<uintptr_t>(d_coef) & 15) != 0 ||
+      (reinterpret_cast<uintptr_t>(d_bits) & 3) != 0)
     return JPEGR_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (hipMemsetAsync(static_cast<uint32_t *>(d_status) + 1, 0, sizeof(uint32_t), s) != hipSuccess)
