@@ -299,22 +299,15 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
       }
       __syncthreads();
     };
-    // the five rounds' entries and segment starts are loaded up front
-    uint32_t meR[5];
-    int begR[5], lenR[5];
+    // pairs owned per entry: the earlier entries of its bucket segment
+    int lenR[5];
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int si = r * 64 + lane;
-      meR[r] = search && si < nk ? S.srt[si] : 0u;
-    }
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int si = r * 64 + lane;
-      begR[r] = 0;
       lenR[r] = 0;
       if (search && si < nk) {
-        begR[r] = (int)bucket_start(S, (meR[r] >> 17) >> (15 - kHB));
-        lenR[r] = si - begR[r];                  // earlier entries of my segment
+        const uint32_t me = S.srt[si];
+        lenR[r] = si - (int)bucket_start(S, (me >> 17) >> (15 - kHB));
       }
     }
     auto pair = [&](uint32_t me, uint32_t o, bool act) {
@@ -327,42 +320,48 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
       S.seq[sl] = (uint32_t)p | ((uint32_t)j << 16);
       ncand += __popcll(cm);
     };
-    // The round's pairs are spread evenly over the lanes: entry e (lane e of
-    // the round) owns pairs [o_e, o_e + len_e) of the round's pair space
-    // (exclusive scan); pair q = base + lane finds its owner through a head
-    // marker (LDS max) and a wave max-scan, then fetches the partner entry.
-    // A round costs ceil(pairs / 64) steps instead of max(len) / 2 (one
-    // large bucket kept most lanes idle: 1,223 lane-slots per text block for
-    // ~138 pairs).  The bucket words double as the 64 head markers here
-    // (bucket starts are already in registers; they are cleared after).
-    uint32_t *head = S.cnt;
+    // The block's pairs are spread evenly over the lanes: entry e owns pairs
+    // [off_e, off_e + len_e) of the block's pair space (exclusive scan over
+    // all entries); pair q = wb + lane of window wb finds its owner through
+    // a head marker ((e + 1) << 7 | position in the window, written by the
+    // owner of the pair that starts there) and a wave max-scan; owners
+    // that started in an earlier window carry over.  ~138 pairs of a text
+    // block take ~3 steps (a per-lane loop over the bucket segment spent
+    // 1,223 lane-slots on them; per-round windows took 5).  The markers live
+    // in the block's not yet written output gap.
+    int offR[5], P = 0;
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-      if (r * 64 >= nk || LZ4R_VARIANT == 3) break;
-      const uint32_t me = meR[r];
-      const int beg = begR[r], len = lenR[r];
-      const uint32_t incl = wave_incl_add((uint32_t)len);
-      const int o = (int)incl - len;
-      const int Pr = (int)lane63(incl);
-      const uint32_t bo = (uint32_t)beg | ((uint32_t)o << 9);      // o < 2^16 (<= 297*296/2)
-      for (int base = 0; base < Pr; base += 64) {
-        head[lane] = 0u;
-        __syncthreads();
-        if (len > 0 && o < base + 64 && o + len > base)
-          atomicMax(&head[o > base ? o - base : 0], (uint32_t)lane + 1u);
-        __syncthreads();
-        const int owner = (int)wave_incl_max(head[lane]) - 1;
-        const int q = base + lane;
-        const bool act = q < Pr;
-        const uint32_t meL = (uint32_t)__shfl((int)me, owner, 64);
-        const uint32_t boL = (uint32_t)__shfl((int)bo, owner, 64);
-        const int k = (int)(boL & 511u) + (q - (int)(boL >> 9));
-        const uint32_t ok = act ? S.srt[k] : 0u;
-        pair(meL, ok, act);
-        if (ncand > kTrash - 64) {
-          drain();
-          ncand = 0;
-        }
+      const uint32_t incl = wave_incl_add((uint32_t)lenR[r]);
+      offR[r] = P + (int)incl - lenR[r];
+      P += (int)lane63(incl);
+    }
+    uint32_t *head = reinterpret_cast<uint32_t *>(S.buf + ((obase + 3) & ~3));
+    int carry_e = 0, carry_d = 0;          // owner continuing into the window, its pair index
+    for (int wb = 0; wb < P && LZ4R_VARIANT != 3; wb += 64) {
+      head[lane] = 0u;
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {
+        const int pos = offR[r] - wb;
+        if (lenR[r] > 0 && pos >= 0 && pos < 64)
+          head[pos] = ((uint32_t)(r * 64 + lane + 1) << 7) | (uint32_t)pos;
+      }
+      __syncthreads();
+      const uint32_t hv = wave_incl_max(head[lane]);
+      const int owner = hv ? (int)(hv >> 7) - 1 : carry_e;
+      const int d = hv ? lane - (int)(hv & 127u) : lane + carry_d;
+      const int q = wb + lane;
+      const bool act = q < P;
+      const uint32_t me = S.srt[owner];
+      const int obeg = (int)bucket_start(S, (me >> 17) >> (15 - kHB));
+      const uint32_t o = act ? S.srt[obeg + d] : 0u;
+      pair(me, o, act);
+      carry_e = (int)lane63((uint32_t)owner);
+      carry_d = (int)lane63((uint32_t)(d + 1));
+      if (ncand > kTrash - 64) {
+        drain();
+        ncand = 0;
       }
     }
     if (ncand) drain();
