@@ -120,18 +120,20 @@ typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned 8-byte LDS acc
 
 // Longest common prefix of the byte runs at a and b (a < b), capped at
 // `limit` = n - b: the canonical clamp (a match never crosses the block end).
-// 8 bytes per step as one unaligned ds_read_b64 per side (the LDS runs in
-// unaligned mode); reads past the region land in its pad.
+// 8-byte words as unaligned ds_read_b64 (the LDS runs in unaligned mode);
+// reads past the region land in its pad (>= 16 B past any block end).
 __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
   int l = 0;
-  while (l < limit) {
-    const uint64_t x = *reinterpret_cast<const u64u *>(d + a + l) ^
-                       *reinterpret_cast<const u64u *>(d + b + l);
-    if (x) {
-      l += __builtin_ctzll(x) >> 3;
+  while (l < limit) {                     // 16 bytes per step: half the loop overhead
+    const uint64_t x0 = *reinterpret_cast<const u64u *>(d + a + l) ^
+                        *reinterpret_cast<const u64u *>(d + b + l);
+    const uint64_t x1 = *reinterpret_cast<const u64u *>(d + a + l + 8) ^
+                        *reinterpret_cast<const u64u *>(d + b + l + 8);
+    if (x0 | x1) {
+      l += x0 ? (__builtin_ctzll(x0) >> 3) : 8 + (__builtin_ctzll(x1) >> 3);
       return l < limit ? l : limit;
     }
-    l += 8;
+    l += 16;
   }
   return limit;
 }
