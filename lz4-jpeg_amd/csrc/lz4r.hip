@@ -253,23 +253,30 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
   }
   __syncthreads();
   if (search) {
-    // exclusive scan of the 512 bucket sizes: lane owns buckets 8l .. 8l+7
-    // (words 4l .. 4l+3, two u16 counters each; starts <= 297 fit in u16)
-    const uint4 a = reinterpret_cast<const uint4 *>(S.cnt)[lane];
-    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+    // exclusive scan of the kH bucket sizes: lane owns kWL consecutive words
+    // (two u16 counters each; starts <= 297 fit in u16)
+    constexpr int kWL = kH / 2 / 64;
+    uint32_t w[kWL];
+#pragma unroll
+    for (int i = 0; i < kWL; i += 4) {
+      const uint4 a = reinterpret_cast<const uint4 *>(S.cnt)[lane * (kWL / 4) + i / 4];
+      w[i] = a.x; w[i + 1] = a.y; w[i + 2] = a.z; w[i + 3] = a.w;
+    }
     uint32_t tot = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) tot += (w[i] & 0xFFFFu) + (w[i] >> 16);
+    for (int i = 0; i < kWL; ++i) tot += (w[i] & 0xFFFFu) + (w[i] >> 16);
     uint32_t run = wave_incl_add(tot) - tot;
-    uint32_t o[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t lo = run;
-      run += w[i] & 0xFFFFu;
-      o[i] = lo | (run << 16);
-      run += w[i] >> 16;
+    for (int i = 0; i < kWL; ++i) {
+      const uint32_t c = w[i], lo = run;
+      run += c & 0xFFFFu;
+      w[i] = lo | (run << 16);
+      run += c >> 16;
     }
-    reinterpret_cast<uint4 *>(S.cnt)[lane] = make_uint4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+    for (int i = 0; i < kWL; i += 4)
+      reinterpret_cast<uint4 *>(S.cnt)[lane * (kWL / 4) + i / 4] =
+          make_uint4(w[i], w[i + 1], w[i + 2], w[i + 3]);
   }
   __syncthreads();
   if (search) {
@@ -368,7 +375,9 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
     }
     if (ncand) drain();
     // reset the bucket counters for the next block
-    reinterpret_cast<uint4 *>(S.cnt)[lane] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < kH / 2 / 64; i += 4)
+      reinterpret_cast<uint4 *>(S.cnt)[lane * (kH / 2 / 256) + i / 4] = make_uint4(0, 0, 0, 0);
   }
   PROF_T(1);
   __syncthreads();
