@@ -32,8 +32,8 @@
 //            walk c0 = nm(0), c_{k+1} = succ(c_k), one LDS read per sequence.
 //     emit   sequence k on lane k: sizes, wave scan for offsets, token /
 //            size / literal-extension / offset bytes (write_sequence,
-//            LZ4.c:365-413), then a position-parallel literal scatter, into
-//            the tile's LDS output (overlaying already-consumed input).
+//            LZ4.c:365-413) and its literal run (16-B unaligned LDS copies),
+//            into the tile's LDS output (overlaying already-consumed input).
 //   store    the tile's bytes -> its 16-B aligned scratch slot, size -> tsz.
 // lz4_scan_reduce / lz4_scan_partials: exclusive scan of tile sizes.
 // lz4_gather: 64 tiles per workgroup, slot -> final offset, 16-B stores.
@@ -51,7 +51,8 @@
 
 // LZ4R_VARIANT (timing ablations only, never shipped): 1 = no match search,
 // 2 = no index/match phase, 3 = index only (no candidates), 4 = candidates
-// without the lcp verification, 6 = input from a 150 KB hot set (isolates the
+// without the lcp verification, 6 = input from a 150 KB hot set, 10 = no
+// literal scatter, 11 = no sequence emission and no literal scatter (isolates the
 // HBM fetch: 7.27 vs 7.00 ms on 1 GiB -- the fetch is hidden by occupancy)
 #ifndef LZ4R_VARIANT
 #define LZ4R_VARIANT 0
@@ -92,19 +93,17 @@ static_assert(kSlot % 16 == 0, "aligned slots");
 
 struct TileLds {
   alignas(16) uint8_t buf[kRegion];
-  // two u16 bucket counters per word, then the bucket starts; afterwards the
-  // visit bytes of the greedy walk (all zero again when the block is done)
+  // two u16 bucket counters per word, then the bucket starts (zero again
+  // when the block is done)
   alignas(16) uint32_t cnt[kH / 2];
   union {
     uint32_t srt[kArr];   // entries sorted by bucket
     uint16_t nm[kArr];    // then: first matchable position >= x
   };
   uint32_t rec[kArr];     // local(p) accumulator; then M | dist<<8 | succ<<17
-  uint32_t seq[kArr];     // candidate list; then per sequence: cpos | end<<16,
-                          // then pend | lit<<9
+  uint32_t seq[kArr];     // candidate list; then per sequence: cpos | end<<16
   uint16_t bsize[kTB];
 };
-static_assert(kH / 2 * 4 >= kArr, "visit bytes fit in the counter words");
 
 __device__ __forceinline__ uint32_t bucket_start(const TileLds &S, uint32_t b) {
   return (S.cnt[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu;
@@ -116,7 +115,9 @@ __device__ __forceinline__ uint32_t load4u(const uint8_t *b, int off) {
   return __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(off & 3));
 }
 
-typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned 8-byte LDS access
+typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned LDS access (the LDS
+typedef uint32_t u32u __attribute__((aligned(1)));   // runs in unaligned mode)
+typedef uint16_t u16u __attribute__((aligned(1)));
 
 // Longest common prefix of the byte runs at a and b (a < b), capped at
 // `limit` = n - b: the canonical clamp (a match never crosses the block end).
@@ -435,30 +436,18 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
   while (c < n) {
     const uint32_t rv = __builtin_amdgcn_readfirstlane(S.rec[c]);
     e = c + (int)(rv & 255u);
-    if (lane == 0) {
-      S.seq[Sv] = (uint32_t)c | ((uint32_t)e << 16);
-      reinterpret_cast<uint8_t *>(S.cnt)[c] = 1;
-    }
+    if (lane == 0) S.seq[Sv] = (uint32_t)c | ((uint32_t)e << 16);
     ++Sv;
     c = (int)(rv >> 17);
   }
   __syncthreads();
-  uint64_t V[5];
-#pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int p = r * 64 + lane;
-    uint8_t *vis = reinterpret_cast<uint8_t *>(S.cnt);
-    const bool v = p < n && vis[p] != 0;
-    V[r] = __ballot(v);
-    if (v) vis[p] = 0;
-  }
   PROF_T(4);
   // ---- sequences: lane kk = sequence kk ------------------------------------
   const int nseq = Sv + (e < n ? 1 : 0);
   int ocar = 3;                      // block header: u8 nseq, u16 size
   int szsum = 0;
   int end_prev = 0;                  // end of the previous round's last match
-  for (int s0 = 0; s0 < nseq; s0 += 64) {
+  for (int s0 = 0; s0 < nseq && LZ4R_VARIANT != 11; s0 += 64) {
     const int kk = s0 + lane;
     const bool act = kk < nseq;
     int M = 0, D = 0, cpos = n, end = n;
@@ -491,8 +480,26 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
         if (rem == 255) { S.buf[o++] = 255; S.buf[o++] = 0; }
         else S.buf[o++] = (uint8_t)rem;
       }
-      S.seq[kk] = (uint32_t)pend | ((uint32_t)(o - pend + 512) << 9);  // literal dest
-      o += L;                                                          // LZ4.c:388
+      // literals (LZ4.c:388): the lane copies its own run, 16 bytes per
+      // step, the last piece exact (8/4/2/1) so no lane writes past its run;
+      // the block's input is never overlaid while its output is written
+      const uint8_t *ls = S.buf + base + pend;
+      for (int i = 0; i < L; i += 16) {
+        uint64_t lo = *reinterpret_cast<const u64u *>(ls + i);
+        const uint64_t hi = *reinterpret_cast<const u64u *>(ls + i + 8);
+        uint8_t *d = S.buf + o + i;
+        const int m = L - i;
+        if (m >= 16) {
+          *reinterpret_cast<u64u *>(d) = lo;
+          *reinterpret_cast<u64u *>(d + 8) = hi;
+          continue;
+        }
+        if (m & 8) { *reinterpret_cast<u64u *>(d) = lo; d += 8; lo = hi; }
+        if (m & 4) { *reinterpret_cast<u32u *>(d) = (uint32_t)lo; d += 4; lo >>= 32; }
+        if (m & 2) { *reinterpret_cast<u16u *>(d) = (uint16_t)lo; d += 2; lo >>= 16; }
+        if (m & 1) *d = (uint8_t)lo;
+      }
+      o += L;
       S.buf[o++] = (uint8_t)(D & 255);                                 // LZ4.c:390
       S.buf[o++] = (uint8_t)((D >> 8) & 255);
       if (M >= 4 && ((M - 4) & 255) >= 15)                             // LZ4.c:393-411
@@ -506,28 +513,9 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
     S.buf[obase] = (uint8_t)nseq;
     S.buf[obase + 1] = (uint8_t)(bsz & 255);
     S.buf[obase + 2] = (uint8_t)((bsz >> 8) & 255);
-    // positions inside a block-final match rank to sequence Sv: when there
-    // is no literal tail, that slot gets pend = n so they are never scattered
-    if (e >= n) S.seq[Sv] = (uint32_t)n;
   }
   __syncthreads();
-
   PROF_T(5);
-  // ---- literal bytes: position-parallel scatter ----------------------------
-  int preV = 0;
-#pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int p = r * 64 + lane;
-    if (p < n && !((V[r] >> lane) & 1ull)) {
-      const int kk = preV + __popcll(V[r] & lanemask_lt());
-      const uint32_t sl = S.seq[kk];
-      const int pend = (int)(sl & 511u);
-      if (p >= pend) S.buf[(int)(sl >> 9) - 512 + p] = (uint8_t)(key[r] & 255u);
-    }
-    preV += __popcll(V[r]);
-  }
-  __syncthreads();
-  PROF_T(6);
   return ocar;
 }
 
