@@ -472,14 +472,17 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
       int o = obase + ocar + excl;
       const int tl = L >= 15 ? 15 : L;                                // LZ4.c:540
       const int tm = M == 0 ? 0 : (M >= 19 ? 15 : ((M - 4) & 255));   // LZ4.c:542
-      S.buf[o++] = (uint8_t)((tl << 4) | tm);                          // LZ4.c:367
-      S.buf[o++] = (uint8_t)(SZ & 255);                                // LZ4.c:369
-      S.buf[o++] = (uint8_t)((SZ >> 8) & 255);
-      if (L >= 15) {                                                   // LZ4.c:372-386
-        const int rem = (L - 15) & 255;
-        if (rem == 255) { S.buf[o++] = 255; S.buf[o++] = 0; }
-        else S.buf[o++] = (uint8_t)rem;
-      }
+      // token, u16 size, literal-extension bytes (LZ4.c:367-386) assembled in
+      // a register and written as one unaligned dword (+ one byte): bytes
+      // past the header are overwritten by the literals / offset after it
+      const int rem = (L - 15) & 255;
+      const int le = L >= 15 ? (rem == 255 ? 2 : 1) : 0;
+      const uint32_t ext = rem == 255 ? 255u : (uint32_t)rem;         // [255, 0] or [rem]
+      const uint64_t hdrw = (uint64_t)((tl << 4) | tm) | ((uint64_t)(SZ & 0xFFFF) << 8) |
+                            ((uint64_t)ext << 24);                    // 5th byte: 0
+      *reinterpret_cast<u32u *>(S.buf + o) = (uint32_t)hdrw;
+      if (le == 2) S.buf[o + 4] = 0;
+      o += 3 + le;
       // literals (LZ4.c:388): the lane copies its own run, 16 bytes per
       // step, the last piece exact (8/4/2/1) so no lane writes past its run;
       // the block's input is never overlaid while its output is written
@@ -500,10 +503,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
         if (m & 1) *d = (uint8_t)lo;
       }
       o += L;
-      S.buf[o++] = (uint8_t)(D & 255);                                 // LZ4.c:390
-      S.buf[o++] = (uint8_t)((D >> 8) & 255);
-      if (M >= 4 && ((M - 4) & 255) >= 15)                             // LZ4.c:393-411
-        S.buf[o++] = (uint8_t)(((M - 4) & 255) - 15);
+      // offset (LZ4.c:390) and match extension (LZ4.c:393-411)
+      const bool mext = M >= 4 && ((M - 4) & 255) >= 15;
+      *reinterpret_cast<u16u *>(S.buf + o) = (uint16_t)D;
+      if (mext) S.buf[o + 2] = (uint8_t)(((M - 4) & 255) - 15);
     }
     ocar += (int)(tot & 0xFFFFu);
     szsum += (int)(tot >> 16);
