@@ -33,7 +33,8 @@
 namespace {
 
 constexpr int kLanes = 64;
-constexpr int kFastCap = 32;             // distinct symbols in the LDS pass
+constexpr int kFastCap = 32;             // distinct symbols in the LDS pass (luma)
+constexpr int kChromaCap = 16;           // ... (chroma)
 constexpr int kFullCap = 128;            // RLE of 64 ints: <= 128 symbols
 constexpr int kPass2Lanes = 64 * 64;     // lanes of the deferred pass
 
@@ -258,14 +259,15 @@ template <typename T>
 using GColT = Col<T>;
 
 // dword-column blocks ([rows][64] u32), rows = elements * size / 4
+template <int Cap>
 struct FastLds {
-  uint32_t sym[kFastCap / 2][kLanes];
-  uint32_t hash[2 * kFastCap / 4][kLanes];
-  uint32_t heap[kFastCap / 2][kLanes];
-  uint32_t child[kFastCap / 2][kLanes];
-  uint32_t code[kFastCap][kLanes];
-  uint32_t len[kFastCap / 4][kLanes];
-  uint32_t stk[(kFastCap + 2) / 2][kLanes];
+  uint32_t sym[Cap / 2][kLanes];
+  uint32_t hash[2 * Cap / 4][kLanes];
+  uint32_t heap[Cap / 2][kLanes];
+  uint32_t child[Cap / 2][kLanes];
+  uint32_t code[Cap][kLanes];
+  uint32_t len[Cap / 4][kLanes];
+  uint32_t stk[(Cap + 2) / 2][kLanes];
 };
 
 // scratch header (in d_scratch): [0] deferred count, then the deferred list
@@ -274,19 +276,24 @@ struct ScratchHdr {
   uint32_t pad[3];
 };
 
+// Luma streams (64 ints, up to ~21 distinct symbols on noise) get room for
+// kFastCap symbols; chroma streams (32 ints, <= ~10) for kChromaCap, half the
+// LDS and so twice the waves per CU.  Streams with more symbols are deferred.
+template <bool kLuma>
 __global__ __launch_bounds__(kLanes) void entropy_encode_fast(
     const int16_t *__restrict__ coef, size_t ntiles, uint8_t *__restrict__ bits,
     uint32_t *__restrict__ meta, uint32_t *__restrict__ table, ScratchHdr *__restrict__ hdr,
     uint32_t *__restrict__ deferred, uint32_t *__restrict__ status) {
-  __shared__ FastLds S;
+  constexpr int Cap = kLuma ? kFastCap : kChromaCap;
+  __shared__ FastLds<Cap> S;
   const int lane = threadIdx.x;
-  const int c = (int)(blockIdx.x % 3);                      // channel of this wave
-  const size_t tile = (size_t)(blockIdx.x / 3) * kLanes + lane;
+  const int c = kLuma ? 0 : 1 + (int)(blockIdx.x & 1);      // channel of this wave
+  const size_t tile = (size_t)(kLuma ? blockIdx.x : blockIdx.x >> 1) * kLanes + lane;
   if (tile >= ntiles) return;
   auto col = [&](uint32_t(*blk)[kLanes]) { return reinterpret_cast<uint8_t *>(&blk[0][lane]); };
   const Work<LCol> w{{col(S.sym)}, {col(S.hash)}, {col(S.heap)}, {col(S.child)},
                      {col(S.code)}, {col(S.len)}, {col(S.stk)}};
-  const int rc = encode_stream<kFastCap>(
+  const int rc = encode_stream<Cap>(
       coef + tile * 128 + coef_off(c), stream_len(c), w, bits + tile * kBitsPerTile + bits_off(c),
       bits_cap(c), ref_bits_max(c), table + tile * kTablePerTile + bits_off(c),
       meta + tile * 3 + c);
@@ -505,7 +512,11 @@ extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, vo
   auto *status = static_cast<uint32_t *>(d_status);
   hipLaunchKernelGGL(entropy_init, dim3(1), dim3(1), 0, s, hdr, status);
   const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
-  hipLaunchKernelGGL(entropy_encode_fast, dim3(groups * 3), dim3(kLanes), 0, s,
+  hipLaunchKernelGGL(entropy_encode_fast<true>, dim3(groups), dim3(kLanes), 0, s,
+                     static_cast<const int16_t *>(d_coef), ntiles, static_cast<uint8_t *>(d_bits),
+                     static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
+                     deferred, status);
+  hipLaunchKernelGGL(entropy_encode_fast<false>, dim3(groups * 2), dim3(kLanes), 0, s,
                      static_cast<const int16_t *>(d_coef), ntiles, static_cast<uint8_t *>(d_bits),
                      static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
                      deferred, status);
