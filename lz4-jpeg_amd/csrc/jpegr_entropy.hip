@@ -343,12 +343,13 @@ constexpr size_t kWorkBytesPerLane = 2 * kFullCap /*sym*/ + 2 * kFullCap /*hash*
 
 // ---- decode ------------------------------------------------------------------
 
-constexpr int kDecCap = 64;                // codes held in LDS (more: read from global)
+constexpr int kDecCap = 32;                // codes held in LDS (more: regenerated per symbol)
 
+template <int N>
 struct DecLds {
   uint32_t lc[kDecCap][kLanes];            // left-aligned codes, increasing
   uint32_t vl[kDecCap][kLanes];            // value | len << 16
-  alignas(16) int16_t out[kLanes][64];     // the lane's decoded ints (leave as 16-B stores)
+  alignas(16) int16_t out[kLanes][N];      // the lane's decoded ints (leave as 16-B stores)
 };
 
 // Decode one stream: bits + table -> RLE ints (decode_huffman) -> n ints
@@ -460,14 +461,16 @@ __device__ bool decode_stream_slow(const uint8_t *__restrict__ bits, uint32_t m,
   return true;
 }
 
+// luma and chroma waves apart, as in the encoder (their output slots differ)
+template <bool kLuma>
 __global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
     const uint8_t *__restrict__ bits, const uint32_t *__restrict__ meta,
     const uint32_t *__restrict__ table, size_t ntiles, int16_t *__restrict__ coef,
     uint32_t *__restrict__ status) {
-  __shared__ DecLds S;
+  __shared__ DecLds<kLuma ? 64 : 32> S;
   const int lane = threadIdx.x;
-  const int c = (int)(blockIdx.x % 3);
-  const size_t tile = (size_t)(blockIdx.x / 3) * kLanes + lane;
+  const int c = kLuma ? 0 : 1 + (int)(blockIdx.x & 1);
+  const size_t tile = (size_t)(kLuma ? blockIdx.x : blockIdx.x >> 1) * kLanes + lane;
   if (tile >= ntiles) return;
   const uint32_t m = meta[tile * 3 + c];
   const int U = (int)(m >> 24);
@@ -538,7 +541,11 @@ extern "C" int jpegr_entropy_decode_device(const void *d_bits, const void *d_met
   if (hipMemsetAsync(static_cast<uint32_t *>(d_status) + 1, 0, sizeof(uint32_t), s) != hipSuccess)
     return JPEGR_ERR_HIP;
   const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
-  hipLaunchKernelGGL(entropy_decode_kernel, dim3(groups * 3), dim3(kLanes), 0, s,
+  hipLaunchKernelGGL(entropy_decode_kernel<true>, dim3(groups), dim3(kLanes), 0, s,
+                     static_cast<const uint8_t *>(d_bits), static_cast<const uint32_t *>(d_meta),
+                     static_cast<const uint32_t *>(d_table), ntiles,
+                     static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
+  hipLaunchKernelGGL(entropy_decode_kernel<false>, dim3(groups * 2), dim3(kLanes), 0, s,
                      static_cast<const uint8_t *>(d_bits), static_cast<const uint32_t *>(d_meta),
                      static_cast<const uint32_t *>(d_table), ntiles,
                      static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
