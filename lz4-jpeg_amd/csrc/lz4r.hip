@@ -8,18 +8,21 @@
 // Blocks are independent; the compressor is one compute kernel plus a cheap
 // placement pass:
 //
-// lz4_tiles: workgroup = one wave = one tile of kTB = 4 consecutive blocks
-// (1,200 B).  Per tile:
-//   stage    tile bytes -> LDS (16-B loads: the only read of the input).
+// lz4_tiles: workgroup = one wave = one tile of kTB consecutive blocks
+// (default 1: 5.1 KB of LDS, <= 64 VGPRs -> 8 waves per SIMD; occupancy is
+// what this issue/latency-bound kernel lives on).  Per tile:
+//   stage    tile bytes -> LDS (widest aligned loads: the only read of the input).
 //   per block, position-parallel (lane owns p = 64r + lane, r < 5):
-//     index  counting sort of the 4-gram starts by a 9-bit hash (LDS
-//            atomicAdd slot, DPP scan of the 512 bucket counts, scatter of
-//            self-describing entries pos | preceding byte << 9 | tag << 17).
-//     local  every unordered pair inside a bucket segment is met once
-//            (independent LDS loads); a pair (j < p) is a candidate when the
-//            tags agree and it is LEFT-MAXIMAL (j == 0 or blk[j-1] !=
-//            blk[p-1]); a balanced lcp pass takes the longest candidate per
-//            p, ties to the smallest j (LDS atomicMax).
+//     index  per-bucket chains of the 4-gram starts by an 8-bit hash: p swaps
+//            itself into its bucket's head (ds_wrxchg) and keeps the old head
+//            as its link; entry = link | preceding byte << 9 | tag << 17.
+//     local  every unordered pair of a bucket is met once, by the later-
+//            inserted entry walking its chain; walkers that go on are
+//            re-queued, so every pass is balanced over the lanes.  A pair
+//            (j < p) is a candidate when the tags agree and it is
+//            LEFT-MAXIMAL (j == 0 or blk[j-1] != blk[p-1]); a balanced lcp
+//            pass takes the longest candidate per p, ties to the smallest j
+//            (LDS atomicMax).
 //     best   a candidate that is not left-maximal is the pair (j-1, p-1)
 //            shifted by one, whose match is one byte longer.  Hence
 //              best(p) = lexmax over q <= p of (q + local_len(q), q - local_j(q))
@@ -33,14 +36,15 @@
 //     emit   sequence k on lane k: sizes, wave scan for offsets, token /
 //            size / literal-extension / offset bytes (write_sequence,
 //            LZ4.c:365-413) and its literal run (16-B unaligned LDS copies),
-//            into the tile's LDS output (overlaying already-consumed input).
-//   store    the tile's bytes -> its 16-B aligned scratch slot, size -> tsz.
-// lz4_scan_reduce / lz4_scan_partials: exclusive scan of tile sizes.
-// lz4_gather: 64 tiles per workgroup, slot -> final offset, 16-B stores.
+//            into the block's LDS output area.
+//     store  the block's bytes -> its 16-B aligned scratch slot (one round of
+//            16-B stores), its size -> usz (u32, for the scan) and bsizes (u16).
+// lz4_scan_reduce / lz4_scan_partials: exclusive scan of the block sizes.
+// lz4_gather: 64 blocks per workgroup, slot -> final offset, 16-B stores.
 // No workgroup ever waits on another (a fused decoupled look-back ran the
 // waves in lock-step at the pace of the slowest tile of each round).
 // HBM traffic per input byte: 1 B read + ~1.03 B written by lz4_tiles, and
-// ~1.03 B read + ~1.03 B written by lz4_gather (+2 B/block of block sizes).
+// ~1.03 B read + ~1.03 B written by lz4_gather (+6 B/block of block sizes).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -73,41 +77,48 @@ __device__ __forceinline__ uint64_t prof_now() {
 namespace {
 
 constexpr int kBlk = LZ4R_BLOCK;          // 300
-constexpr int kTB = 4;                    // blocks per tile
-constexpr int kTileIn = kTB * kBlk;       // 2400 B, multiple of 16
-constexpr int kBlkOutMax = 600;           // >= 548: worst-case bytes of one block
-// The tile's output grows from buf[0]; block k's input sits at
-// kInOff + 300k.  Writing block k's bytes never reaches its own input:
-// (k+1)*kBlkOutMax <= kInOff + 300k for k < kTB.
-constexpr int kInOff = ((kTB * kBlkOutMax - (kTB - 1) * kBlk) + 15) / 16 * 16;
+#ifndef LZ4R_TB
+#define LZ4R_TB 1
+#endif
+constexpr int kTB = LZ4R_TB;              // blocks per tile
+#ifndef LZ4R_WPE
+#define LZ4R_WPE
+#endif
+constexpr int kTileIn = kTB * kBlk;       // staged input bytes per tile
+constexpr int kBlkOutMax = 560;           // >= 548: worst-case bytes of one block, 16-B multiple
+// LDS byte region: the block being encoded writes its bytes at buf[0 ..
+// kBlkOutMax); the tile's input sits at kInOff + 300k; then an over-read pad.
+constexpr int kInOff = kBlkOutMax;
 constexpr int kRegion = kInOff + kTileIn + 48;  // + over-read pad (lcp, 32-B copy reads)
-constexpr int kHB = 9;                    // hash bits: 512 buckets
+#ifndef LZ4R_HB
+#define LZ4R_HB 8
+#endif
+constexpr int kHB = LZ4R_HB;              // hash bits: 512 buckets
 constexpr int kH = 1 << kHB;
 constexpr int kArr = kBlk + 4;
+constexpr int kQ = kBlk;                 // walker ring (<= one live walker per entry)
+constexpr int kCand = 128;               // candidate list (drained when a pass could fill it)
 
-static_assert((kTB - 1) * kBlk + kInOff >= kTB * kBlkOutMax, "output overlay bound");
-static_assert(kInOff % 16 == 0 && kTileIn % 16 == 0, "16-B staging");
+static_assert(kInOff % 16 == 0 && kTileIn % 4 == 0, "4/8/16-B staging");
 
-constexpr int kSlot = kTB * kBlkOutMax;   // scratch bytes per tile (16-B multiple)
-static_assert(kSlot % 16 == 0, "aligned slots");
+constexpr int kSlot = kBlkOutMax;         // scratch bytes per block slot (16-B multiple)
+static_assert(kSlot % 16 == 0 && kBlkOutMax / 16 <= 64, "aligned slots, one store round");
 
 struct TileLds {
   alignas(16) uint8_t buf[kRegion];
-  // two u16 bucket counters per word, then the bucket starts (zero again
-  // when the block is done)
-  alignas(16) uint32_t cnt[kH / 2];
   union {
-    uint32_t srt[kArr];   // entries sorted by bucket
+    uint32_t head[kH];    // bucket -> 1 + last inserted position (0: empty)
+    uint32_t q[kQ];       // then: chain walkers, walker | next chain entry << 16
+    uint32_t seq[kArr];   // then: per sequence, cpos | end << 16
+  };
+  union {
+    uint32_t ent[kArr];   // per position: link | preceding byte << 9 | tag << 17
     uint16_t nm[kArr];    // then: first matchable position >= x
   };
   uint32_t rec[kArr];     // local(p) accumulator; then M | dist<<8 | succ<<17
-  uint32_t seq[kArr];     // candidate list; then per sequence: cpos | end<<16
-  uint16_t bsize[kTB];
+  uint32_t cand[kCand];   // candidate pairs p | j << 16 awaiting the lcp pass
 };
 
-__device__ __forceinline__ uint32_t bucket_start(const TileLds &S, uint32_t b) {
-  return (S.cnt[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu;
-}
 
 __device__ __forceinline__ uint32_t load4u(const uint8_t *b, int off) {
   const uint32_t *d = reinterpret_cast<const uint32_t *>(b);
@@ -220,165 +231,113 @@ __device__ __forceinline__ uint4 funnel16(uint4 lo, uint4 hi, int sb) {
 
 // Encode block `k` of the tile (n bytes at S.buf[kInOff + 300k]) into
 // S.buf[obase ...]; returns the bytes written.
-__device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
+__device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
                                             uint64_t *prof, uint64_t &prof_last) {
   (void)prof; (void)prof_last;
   const int lane = threadIdx.x;
   const int base = kInOff + k * kBlk;
+  constexpr int obase = 0;
 
-  // ---- index: counting sort of the 4-gram starts by hash bucket -----------
-  // entry = position | preceding byte << 9 | 15-bit hash tag << 17; the
-  // bucket is the tag's top 9 bits, so equal tags imply equal buckets.
-  uint32_t key[5], ent[5], hb[5], slot[5];
+  // ---- index: per-bucket chains of the 4-gram starts -----------------------
+  // Position p swaps itself (+1) into its bucket's head and keeps the
+  // previous head as its link.  The chains are in insertion order: rounds
+  // ascend, and lanes of one round that share a bucket are chained in the
+  // order the LDS served their swaps.  Entry:
+  //   link (9 bits, 511 = none) | preceding byte << 9 | 15-bit hash tag << 17.
+  // Every unordered pair of a bucket is met once, by the later-inserted of
+  // the two walking its chain; walkers that continue are re-queued, so each
+  // pass over the queue is balanced over the lanes whatever the chain lengths.
+  const bool search = LZ4R_VARIANT != 1 && LZ4R_VARIANT != 2;
+  const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
+  static_assert(kH % 256 == 0, "head reset: 16-B stores");
+#pragma unroll
+  for (int i = 0; i < kH / 256; ++i)      // empty heads (the previous block's queue)
+    reinterpret_cast<uint4 *>(S.head)[i * 64 + lane] = make_uint4(0, 0, 0, 0);
+  uint32_t item[5];
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     const int p = r * 64 + lane;
-    key[r] = p < n ? load4u(S.buf, base + p) : 0u;
-    const uint32_t pb = p >= 1 && p < n ? (uint32_t)S.buf[base + p - 1] : 0u;
-    const uint32_t tag = (key[r] * 2654435761u) >> 17;
-    hb[r] = tag >> (15 - kHB);
-    ent[r] = (uint32_t)p | (pb << 9) | (tag << 17);
     if (p < n) S.rec[p] = 0u;            // local(p) accumulator
-  }
-  const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
-  const bool search = LZ4R_VARIANT != 1 && LZ4R_VARIANT != 2;
-  if (search) {
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int p = r * 64 + lane;
-      if (p < nk) {
-        const uint32_t sh = (hb[r] & 1u) * 16;
-        slot[r] = (atomicAdd(&S.cnt[hb[r] >> 1], 1u << sh) >> sh) & 0xFFFFu;
-      }
+    item[r] = 0u;
+    if (search && p < nk) {
+      const uint32_t key = load4u(S.buf, base + p);
+      const uint32_t pb = p >= 1 ? (uint32_t)S.buf[base + p - 1] : 0u;
+      const uint32_t tag = (key * 2654435761u) >> 17;
+      const uint32_t old = atomicExch(&S.head[tag >> (15 - kHB)], (uint32_t)p + 1u);
+      const uint32_t link = old ? old - 1u : 511u;
+      S.ent[p] = link | (pb << 9) | (tag << 17);
+      item[r] = old ? (uint32_t)p | (link << 16) : 0u;
     }
   }
-  __syncthreads();
-  if (search) {
-    // exclusive scan of the kH bucket sizes: lane owns kWL consecutive words
-    // (two u16 counters each; starts <= 297 fit in u16)
-    constexpr int kWL = kH / 2 / 64;
-    uint32_t w[kWL];
+  __syncthreads();                       // the heads are dead: the queue overlays them
+  int qwr = 0;                           // walkers queued (S.q[0 .. qwr))
 #pragma unroll
-    for (int i = 0; i < kWL; i += 4) {
-      const uint4 a = reinterpret_cast<const uint4 *>(S.cnt)[lane * (kWL / 4) + i / 4];
-      w[i] = a.x; w[i + 1] = a.y; w[i + 2] = a.z; w[i + 3] = a.w;
-    }
-    uint32_t tot = 0;
-#pragma unroll
-    for (int i = 0; i < kWL; ++i) tot += (w[i] & 0xFFFFu) + (w[i] >> 16);
-    uint32_t run = wave_incl_add(tot) - tot;
-#pragma unroll
-    for (int i = 0; i < kWL; ++i) {
-      const uint32_t c = w[i], lo = run;
-      run += c & 0xFFFFu;
-      w[i] = lo | (run << 16);
-      run += c >> 16;
-    }
-#pragma unroll
-    for (int i = 0; i < kWL; i += 4)
-      reinterpret_cast<uint4 *>(S.cnt)[lane * (kWL / 4) + i / 4] =
-          make_uint4(w[i], w[i + 1], w[i + 2], w[i + 3]);
-  }
-  __syncthreads();
-  if (search) {
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int p = r * 64 + lane;
-      if (p < nk) S.srt[bucket_start(S, hb[r]) + slot[r]] = ent[r];
-    }
+  for (int r = 0; r < 5; ++r) {
+    const bool walk = item[r] != 0u;     // p != link, so a walker's item is never 0
+    const uint64_t wm = __ballot(walk);
+    if (walk) S.q[qwr + __popcll(wm & lanemask_lt())] = item[r];
+    qwr += __popcll(wm);
   }
   __syncthreads();
 
   PROF_T(0);
-  // ---- candidates: every unordered pair inside a bucket segment, once -------
-  // Lane owns sorted entry s and meets every earlier entry of its segment
-  // (independent loads).  A pair is a candidate when the tags agree and the
-  // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]): (j, p) with
-  // p = the later position, j = the earlier.  Candidates go to a list in
-  // S.seq, drained by a balanced lcp pass with LDS atomicMax into S.rec.
-  {
-    constexpr int kTrash = kArr - 1;
+  // ---- candidates: walk the chains ------------------------------------------
+  // A pair (j < p) of one bucket is a candidate when the tags agree and the
+  // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]).  Candidates go to
+  // a list in S.cand, drained by a balanced lcp pass with LDS atomicMax into
+  // S.rec (len << 9 | 511 - j: the longest, ties to the smallest j).
+  if (search && LZ4R_VARIANT != 3) {
+    constexpr int kTrash = kCand - 1;
     int ncand = 0;
     auto drain = [&]() {
       __syncthreads();
       for (int i = lane; i < ncand && LZ4R_VARIANT != 4; i += 64) {
-        const uint32_t pr = S.seq[i];
+        const uint32_t pr = S.cand[i];
         const int p = (int)(pr & 0xFFFFu), j = (int)(pr >> 16);
         const int l = lcp(S.buf, base + j, base + p, n - p);
         if (l >= 4) atomicMax(&S.rec[p], ((uint32_t)l << 9) | (uint32_t)(511 - j));
       }
       __syncthreads();
     };
-    // pairs owned per entry: the earlier entries of its bucket segment
-    int lenR[5];
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int si = r * 64 + lane;
-      lenR[r] = 0;
-      if (search && si < nk) {
-        const uint32_t me = S.srt[si];
-        lenR[r] = si - (int)bucket_start(S, (me >> 17) >> (15 - kHB));
-      }
-    }
-    auto pair = [&](uint32_t me, uint32_t o, bool act) {
-      const uint32_t x = o ^ me;
-      const int pa = (int)(me & 511u), pj = (int)(o & 511u);
-      const int p = max(pa, pj), j = min(pa, pj);
+    // ring of walkers: a pass reads up to 64, then queues those that go on
+    // (at most one walker per entry is ever live: <= kQ)
+    int qrd = 0, live = qwr;
+    qwr = qwr == kQ ? 0 : qwr;
+    while (live > 0) {
+      const int m = live < 64 ? live : 64;
+      const bool act = lane < m;
+      int qi = qrd + lane;
+      qi -= qi >= kQ ? kQ : 0;
+      const uint32_t it = act ? S.q[qi] : 0u;
+      const int a = (int)(it & 0xFFFFu), b = (int)(it >> 16);   // a walks, b < ... in chain
+      const uint32_t me = S.ent[a], o = S.ent[b];
+      const uint32_t x = me ^ o;
+      const int p = max(a, b), j = min(a, b);
       const bool cand = act && (x >> 17) == 0 && (j == 0 || (x & (255u << 9)) != 0);
       const uint64_t cm = __ballot(cand);
       const int sl = cand ? ncand + __popcll(cm & lanemask_lt()) : kTrash;
-      S.seq[sl] = (uint32_t)p | ((uint32_t)j << 16);
+      S.cand[sl] = (uint32_t)p | ((uint32_t)j << 16);
       ncand += __popcll(cm);
-    };
-    // The block's pairs are spread evenly over the lanes: entry e owns pairs
-    // [off_e, off_e + len_e) of the block's pair space (exclusive scan over
-    // all entries); pair q = wb + lane of window wb finds its owner through
-    // a head marker ((e + 1) << 7 | position in the window, written by the
-    // owner of the pair that starts there) and a wave max-scan; owners
-    // that started in an earlier window carry over.  ~138 pairs of a text
-    // block take ~3 steps (a per-lane loop over the bucket segment spent
-    // 1,223 lane-slots on them; per-round windows took 5).  The markers live
-    // in the block's not yet written output gap.
-    int offR[5], P = 0;
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const uint32_t incl = wave_incl_add((uint32_t)lenR[r]);
-      offR[r] = P + (int)incl - lenR[r];
-      P += (int)lane63(incl);
-    }
-    uint32_t *head = reinterpret_cast<uint32_t *>(S.buf + ((obase + 3) & ~3));
-    int carry_e = 0, carry_d = 0;          // owner continuing into the window, its pair index
-    for (int wb = 0; wb < P && LZ4R_VARIANT != 3; wb += 64) {
-      head[lane] = 0u;
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < 5; ++r) {
-        const int pos = offR[r] - wb;
-        if (lenR[r] > 0 && pos >= 0 && pos < 64)
-          head[pos] = ((uint32_t)(r * 64 + lane + 1) << 7) | (uint32_t)pos;
+      const uint32_t nx = o & 511u;
+      const bool go = act && nx != 511u;
+      const uint64_t gm = __ballot(go);
+      if (go) {
+        int wi = qwr + __popcll(gm & lanemask_lt());
+        wi -= wi >= kQ ? kQ : 0;
+        S.q[wi] = (uint32_t)a | (nx << 16);
       }
-      __syncthreads();
-      const uint32_t hv = wave_incl_max(head[lane]);
-      const int owner = hv ? (int)(hv >> 7) - 1 : carry_e;
-      const int d = hv ? lane - (int)(hv & 127u) : lane + carry_d;
-      const int q = wb + lane;
-      const bool act = q < P;
-      const uint32_t me = S.srt[owner];
-      const int obeg = (int)bucket_start(S, (me >> 17) >> (15 - kHB));
-      const uint32_t o = act ? S.srt[obeg + d] : 0u;
-      pair(me, o, act);
-      carry_e = (int)lane63((uint32_t)owner);
-      carry_d = (int)lane63((uint32_t)(d + 1));
+      const int ng = __popcll(gm);
+      qrd += m;
+      qrd -= qrd >= kQ ? kQ : 0;
+      qwr += ng;
+      qwr -= qwr >= kQ ? kQ : 0;
+      live += ng - m;
       if (ncand > kTrash - 64) {
         drain();
         ncand = 0;
       }
     }
     if (ncand) drain();
-    // reset the bucket counters for the next block
-#pragma unroll
-    for (int i = 0; i < kH / 2 / 64; i += 4)
-      reinterpret_cast<uint4 *>(S.cnt)[lane * (kH / 2 / 256) + i / 4] = make_uint4(0, 0, 0, 0);
   }
   PROF_T(1);
   __syncthreads();
@@ -522,9 +481,9 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n, int obase,
   return ocar;
 }
 
-__global__ __launch_bounds__(64) void lz4_tiles(
+__global__ __launch_bounds__(64) LZ4R_WPE void lz4_tiles(
     const uint8_t *__restrict__ in, size_t n_total, size_t nb_total, size_t ntiles,
-    uint8_t *__restrict__ slots, uint32_t *__restrict__ tsz,
+    uint8_t *__restrict__ slots, uint32_t *__restrict__ usz,
     uint16_t *__restrict__ bsizes) {
   __shared__ TileLds S;
   const int lane = threadIdx.x;
@@ -534,8 +493,6 @@ __global__ __launch_bounds__(64) void lz4_tiles(
 #else
   uint64_t prof_last = 0;
 #endif
-
-  for (int i = lane; i < kH / 2; i += 64) S.cnt[i] = 0u;
 
   for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const size_t b0 = t * kTB;
@@ -549,35 +506,44 @@ __global__ __launch_bounds__(64) void lz4_tiles(
     // ---- stage the tile (16-B loads) ---------------------------------------
     {
       uint8_t *dst = S.buf + kInOff;
-      const int nvec = (((uintptr_t)src & 15) == 0) ? (len >> 4) : 0;
-      for (int i = lane; i < nvec; i += 64)
-        reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
-      for (int i = nvec * 16 + lane; i < len; i += 64) dst[i] = src[i];
+      int done = 0;
+      if (((uintptr_t)src & 15) == 0) {
+        const int nvec = len >> 4;
+        for (int i = lane; i < nvec; i += 64)
+          reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+        done = nvec * 16;
+      } else if (((uintptr_t)src & 7) == 0) {   // 2-block tiles start 8-B aligned
+        const int nvec = len >> 3;
+        for (int i = lane; i < nvec; i += 64)
+          reinterpret_cast<uint2 *>(dst)[i] = reinterpret_cast<const uint2 *>(src)[i];
+        done = nvec * 8;
+      } else if (((uintptr_t)src & 3) == 0) {   // 1-block tiles start 4-B aligned
+        const int nvec = len >> 2;
+        for (int i = lane; i < nvec; i += 64)
+          reinterpret_cast<uint32_t *>(dst)[i] = reinterpret_cast<const uint32_t *>(src)[i];
+        done = nvec * 4;
+      }
+      for (int i = done + lane; i < len; i += 64) dst[i] = src[i];
       if (lane < 16) dst[len + lane] = 0;
     }
     __syncthreads();
 
-    // ---- encode the tile's blocks ------------------------------------------
-    int obase = 0;
+    // ---- encode the tile's blocks; each leaves for its slot at once ---------
     for (int k = 0; k < nbt; ++k) {
       const size_t gb = b0 + k;
       const int n = (gb == nb_total - 1) ? (int)(n_total - gb * kBlk) : kBlk;
       PROF_T(7);
-      const int W = encode_block(S, k, n, obase, prof, prof_last);
-      if (lane == 0) S.bsize[k] = (uint16_t)W;
-      obase += W;
-    }
-    __syncthreads();
-    if (lane < nbt) bsizes[b0 + lane] = S.bsize[lane];
-
-    PROF_T(8);
-    // ---- store: the tile's bytes to its 16-B aligned scratch slot ----------
-    {
-      uint4 *dst = reinterpret_cast<uint4 *>(slots + t * (size_t)kSlot);
-      const int nchunks = (obase + 15) >> 4;
-      for (int ci = lane; ci < nchunks; ci += 64)
-        dst[ci] = reinterpret_cast<const uint4 *>(S.buf)[ci];
-      if (lane == 0) tsz[t] = (uint32_t)obase;
+      const int W = encode_block(S, k, n, prof, prof_last);
+      PROF_T(8);
+      // the block's bytes -> its 16-B aligned slot (<= 35 chunks: one round);
+      // the next block overwrites buf[0 ..) only after these LDS reads (in order)
+      uint4 *dst = reinterpret_cast<uint4 *>(slots + gb * (size_t)kSlot);
+      if (lane < ((W + 15) >> 4)) dst[lane] = reinterpret_cast<const uint4 *>(S.buf)[lane];
+      if (lane == 0) {
+        usz[gb] = (uint32_t)W;
+        bsizes[gb] = (uint16_t)W;
+      }
+      PROF_T(9);
     }
     __syncthreads();                                // LDS reused by the next tile
     PROF_T(9);
@@ -668,8 +634,9 @@ __device__ __forceinline__ uint4 select16(uint4 x, uint4 y, int k) {
 
 // Workgroup = group of 64 consecutive tiles.  Offsets from the partials,
 // the group sums and a wave scan; then the group's output range is written
-// as aligned 16-B chunks, each assembled from at most two tiles' slots (a
-// tile is >= 32 B except the globally last).  Only the group's two edge
+// as aligned 16-B chunks, each assembled from at most two blocks' slots (a
+// full 300-B block encodes to >= 16 B: p = 0 is a literal, so it takes two
+// sequences, 3 + 7 + 6 bytes at the least; only the globally last is shorter).  Only the group's two edge
 // chunks are written bytewise.  Also writes the frame byte (LZ4.c:429).
 __global__ __launch_bounds__(256) void lz4_gather(
     const uint8_t *__restrict__ slots, const uint32_t *__restrict__ tsz, size_t ntiles,
@@ -731,10 +698,9 @@ __global__ __launch_bounds__(256) void lz4_gather(
 struct lz4r_ctx {
   int device = 0;
   size_t cap_blocks = 0;       // capacity of the per-block arrays
-  size_t cap_tiles = 0;
   uint16_t *bsizes = nullptr;  // encoded bytes of every block of the last call
-  uint8_t *slots = nullptr;    // per-tile output slots (kSlot bytes each)
-  uint32_t *tsz = nullptr;     // encoded bytes per tile
+  uint8_t *slots = nullptr;    // per-block output slots (kSlot bytes each)
+  uint32_t *tsz = nullptr;     // encoded bytes per block (u32, for the scan)
   uint32_t *gsum = nullptr;    // encoded bytes per group of kGT tiles
   uint64_t *part = nullptr;    // scan partials, one per kPart tiles
   unsigned max_grid = 0;       // resident workgroups of lz4_tiles on this device
@@ -759,31 +725,28 @@ void free_scratch(lz4r_ctx *c) {
   c->gsum = nullptr;
   c->part = nullptr;
   c->cap_blocks = 0;
-  c->cap_tiles = 0;
 }
 
 int ensure_scratch(lz4r_ctx *c, size_t nb) {
   if (nb <= c->cap_blocks) return LZ4R_OK;
   free_scratch(c);
   const size_t cap = nb + nb / 8 + 1024;
-  const size_t tiles = (cap + kTB - 1) / kTB;
-  const size_t parts = (tiles + kPart - 1) / kPart;
-  const size_t groups = (tiles + kGT - 1) / kGT;
+  const size_t parts = (cap + kPart - 1) / kPart;
+  const size_t groups = (cap + kGT - 1) / kGT;
   uint8_t *slots = nullptr;      // 16-B pad in front: gather reads slot - 16
-  if (hipMalloc(&slots, tiles * (size_t)kSlot + 32) != hipSuccess) {
+  if (hipMalloc(&slots, cap * (size_t)kSlot + 32) != hipSuccess) {
     free_scratch(c);
     return LZ4R_ERR_NOMEM;
   }
   c->slots = slots + 16;
   if (hipMalloc(&c->bsizes, cap * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&c->tsz, tiles * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&c->tsz, cap * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&c->gsum, groups * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&c->part, parts * sizeof(uint64_t)) != hipSuccess) {
     free_scratch(c);
     return LZ4R_ERR_NOMEM;
   }
   c->cap_blocks = cap;
-  c->cap_tiles = tiles;
   return LZ4R_OK;
 }
 
@@ -796,7 +759,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   int rc = ensure_scratch(c, nb);
   if (rc != LZ4R_OK) return rc;
   const size_t ntiles = (nb + kTB - 1) / kTB;
-  if (ntiles > 0xffffffffULL || n > (1ull << 37)) return LZ4R_ERR_ARG;
+  if (nb > 0xffffffffULL || n > (1ull << 37)) return LZ4R_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool timed = c->timing;
   c->timed_call = timed;
@@ -807,13 +770,13 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
                      static_cast<const uint8_t *>(d_in), n, nb, ntiles, c->slots, c->tsz,
                      c->bsizes);
   if (timed) (void)hipEventRecord(c->ev_b, s);
-  const size_t nparts = (ntiles + kPart - 1) / kPart;
-  hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)nparts), dim3(256), 0, s, c->tsz, ntiles,
+  const size_t nparts = (nb + kPart - 1) / kPart;
+  hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)nparts), dim3(256), 0, s, c->tsz, nb,
                      c->gsum, c->part);
   hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part, nparts,
                      (uint64_t)hdr, static_cast<uint64_t *>(d_len));
-  hipLaunchKernelGGL(lz4_gather, dim3((unsigned)((ntiles + kGT - 1) / kGT)), dim3(256), 0, s,
-                     c->slots, c->tsz, ntiles, c->gsum, c->part,
+  hipLaunchKernelGGL(lz4_gather, dim3((unsigned)((nb + kGT - 1) / kGT)), dim3(256), 0, s,
+                     c->slots, c->tsz, nb, c->gsum, c->part,
                      static_cast<uint8_t *>(d_out), (uint64_t)cap, hdr, (uint64_t)nb);
   if (timed) (void)hipEventRecord(c->ev_c, s);
   c->last_nb = nb;
