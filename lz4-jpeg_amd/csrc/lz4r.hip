@@ -666,8 +666,20 @@ __global__ __launch_bounds__(256) void lz4_gather(
   const uintptr_t abs0 = (uintptr_t)(out + G0), absend = (uintptr_t)(out + G1);
   const uintptr_t first = abs0 & ~(uintptr_t)15;
   const long nchunks = (long)((absend - first + 15) >> 4);
-  int t = 0;                                       // tile cursor (chunks ascend per thread)
-  for (long ci = tid; ci < nchunks; ci += 256) {
+  // each wave takes a contiguous quarter of the chunks, 64 at a time, so a
+  // lane's block cursor moves ~3 blocks per step (a 256-chunk stride moved ~13)
+  const long per = ((nchunks + 255) >> 8) << 6;
+  const long c0 = (long)(tid >> 6) * per, c1 = min(nchunks, c0 + per);
+  int t = 0;                                       // block cursor (chunks ascend per lane)
+  if (c0 + (tid & 63) < c1) {                      // start: largest t with toff[t] <= first chunk
+    const uint64_t oa = (uint64_t)(first + ((uintptr_t)(c0 + (tid & 63)) << 4) - (uintptr_t)out);
+    int hi = nt - 1;
+    while (t < hi) {
+      const int mid = (t + hi + 1) >> 1;
+      if (toff[mid] <= oa) t = mid; else hi = mid - 1;
+    }
+  }
+  for (long ci = c0 + (tid & 63); ci < c1; ci += 64) {
     const uintptr_t a = first + ((uintptr_t)ci << 4);
     const uint64_t oa = (uint64_t)(a - (uintptr_t)out);   // stream offset of the chunk
     const uint64_t ob = oa < G0 ? G0 : oa;
