@@ -13,9 +13,10 @@
 // what this issue/latency-bound kernel lives on).  Per tile:
 //   stage    tile bytes -> LDS (widest aligned loads: the only read of the input).
 //   per block, position-parallel (lane owns p = 64r + lane, r < 5):
-//     index  per-bucket chains of the 4-gram starts by an 8-bit hash: p swaps
-//            itself into its bucket's head (ds_wrxchg) and keeps the old head
-//            as its link; entry = link | preceding byte << 9 | tag << 17.
+//     index  per-bucket chains of the 4-gram starts by a 9-bit hash: p swaps
+//            itself into its bucket's u16 head (ds_mskor_rtn_b32 on a dword of
+//            two heads) and keeps the old head as its link;
+//            entry = link | preceding byte << 9 | tag << 17.
 //     local  every unordered pair of a bucket is met once, by the later-
 //            inserted entry walking its chain; walkers that go on are
 //            re-queued, so every pass is balanced over the lanes.  A pair
@@ -40,14 +41,17 @@
 //     store  the block's bytes -> its 16-B aligned scratch slot (one round of
 //            16-B stores), its size -> usz (u32, for the scan) and bsizes (u16).
 // lz4_scan_reduce / lz4_scan_partials: exclusive scan of the block sizes.
-// lz4_gather: 64 blocks per workgroup, slot -> final offset, 16-B stores.
+// lz4_gather: 32 blocks per workgroup: slots -> LDS image of the output
+// range (unaligned LDS stores) -> aligned 16-B global stores.
 // No workgroup ever waits on another (a fused decoupled look-back ran the
 // waves in lock-step at the pace of the slowest tile of each round).
 // HBM traffic per input byte: 1 B read + ~1.03 B written by lz4_tiles, and
 // ~1.03 B read + ~1.03 B written by lz4_gather (+6 B/block of block sizes).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -90,8 +94,11 @@ constexpr int kBlkOutMax = 560;           // >= 548: worst-case bytes of one blo
 // kBlkOutMax); the tile's input sits at kInOff + 300k; then an over-read pad.
 constexpr int kInOff = kBlkOutMax;
 constexpr int kRegion = kInOff + kTileIn + 48;  // + over-read pad (lcp, 32-B copy reads)
+#ifndef LZ4R_HEAD16
+#define LZ4R_HEAD16 1
+#endif
 #ifndef LZ4R_HB
-#define LZ4R_HB 8
+#define LZ4R_HB (LZ4R_HEAD16 ? 9 : 8)
 #endif
 constexpr int kHB = LZ4R_HB;              // hash bits: 512 buckets
 constexpr int kH = 1 << kHB;
@@ -107,7 +114,11 @@ static_assert(kSlot % 16 == 0 && kBlkOutMax / 16 <= 64, "aligned slots, one stor
 struct TileLds {
   alignas(16) uint8_t buf[kRegion];
   union {
+#if LZ4R_HEAD16
+    uint32_t head[kH / 2];  // bucket -> 1 + last inserted position (0: empty), u16 pairs
+#else
     uint32_t head[kH];    // bucket -> 1 + last inserted position (0: empty)
+#endif
     uint32_t q[kQ];       // then: chain walkers, walker | next chain entry << 16
     uint32_t seq[kArr];   // then: per sequence, cpos | end << 16
   };
@@ -124,6 +135,17 @@ __device__ __forceinline__ uint32_t load4u(const uint8_t *b, int off) {
   const uint32_t *d = reinterpret_cast<const uint32_t *>(b);
   const uint32_t w0 = d[off >> 2], w1 = d[(off >> 2) + 1];
   return __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(off & 3));
+}
+
+// ds_mskor_rtn_b32: *a = (*a & ~clear) | set, returns the old dword (one LDS
+// atomic: a 16-bit exchange inside a dword of two bucket heads)
+__device__ __forceinline__ uint32_t mskor_rtn(uint32_t *a, uint32_t clear, uint32_t set) {
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  const uint32_t off = (uint32_t)(uintptr_t)(lds_u32 *)a;
+  uint32_t old;
+  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(old) : "v"(off), "v"(clear), "v"(set) : "memory");
+  return old;
 }
 
 typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned LDS access (the LDS
@@ -211,22 +233,6 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return (1ull << lane) - 1ull;
 }
 
-// 16 bytes starting at byte `sb` (0..15, wave-uniform) of the 32-byte run lo:hi
-__device__ __forceinline__ uint4 funnel16(uint4 lo, uint4 hi, int sb) {
-  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  const uint32_t by = (uint32_t)(sb & 3);
-  uint32_t x[5];
-  switch (sb >> 2) {
-    case 0: x[0] = w[0]; x[1] = w[1]; x[2] = w[2]; x[3] = w[3]; x[4] = w[4]; break;
-    case 1: x[0] = w[1]; x[1] = w[2]; x[2] = w[3]; x[3] = w[4]; x[4] = w[5]; break;
-    case 2: x[0] = w[2]; x[1] = w[3]; x[2] = w[4]; x[3] = w[5]; x[4] = w[6]; break;
-    default: x[0] = w[3]; x[1] = w[4]; x[2] = w[5]; x[3] = w[6]; x[4] = w[7]; break;
-  }
-  return make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], by),
-                    __builtin_amdgcn_alignbyte(x[2], x[1], by),
-                    __builtin_amdgcn_alignbyte(x[3], x[2], by),
-                    __builtin_amdgcn_alignbyte(x[4], x[3], by));
-}
 
 
 // Encode block `k` of the tile (n bytes at S.buf[kInOff + 300k]) into
@@ -249,9 +255,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
   // pass over the queue is balanced over the lanes whatever the chain lengths.
   const bool search = LZ4R_VARIANT != 1 && LZ4R_VARIANT != 2;
   const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
-  static_assert(kH % 256 == 0, "head reset: 16-B stores");
+  constexpr int kHeadW = LZ4R_HEAD16 ? kH / 2 : kH;   // head dwords
+  static_assert(kHeadW % 256 == 0, "head reset: 16-B stores");
 #pragma unroll
-  for (int i = 0; i < kH / 256; ++i)      // empty heads (the previous block's queue)
+  for (int i = 0; i < kHeadW / 256; ++i)  // empty heads (the previous block's queue)
     reinterpret_cast<uint4 *>(S.head)[i * 64 + lane] = make_uint4(0, 0, 0, 0);
   uint32_t item[5];
 #pragma unroll
@@ -263,7 +270,12 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
       const uint32_t key = load4u(S.buf, base + p);
       const uint32_t pb = p >= 1 ? (uint32_t)S.buf[base + p - 1] : 0u;
       const uint32_t tag = (key * 2654435761u) >> 17;
+#if LZ4R_HEAD16
+      const uint32_t bk = tag >> (15 - kHB), sh = (bk & 1u) << 4;
+      const uint32_t old = mskor_rtn(&S.head[bk >> 1], 0xFFFFu << sh, ((uint32_t)p + 1u) << sh) >> sh & 0xFFFFu;
+#else
       const uint32_t old = atomicExch(&S.head[tag >> (15 - kHB)], (uint32_t)p + 1u);
+#endif
       const uint32_t link = old ? old - 1u : 511u;
       S.ent[p] = link | (pb << 9) | (tag << 17);
       item[r] = old ? (uint32_t)p | (link << 16) : 0u;
@@ -482,8 +494,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
 }
 
 __global__ __launch_bounds__(64) LZ4R_WPE void lz4_tiles(
-    const uint8_t *__restrict__ in, size_t n_total, size_t nb_total, size_t ntiles,
-    uint8_t *__restrict__ slots, uint32_t *__restrict__ usz,
+    const uint8_t *__restrict__ in, size_t n_total, size_t nb_total, size_t t_first,
+    size_t ntiles, uint8_t *__restrict__ slots, uint32_t *__restrict__ usz,
     uint16_t *__restrict__ bsizes) {
   __shared__ TileLds S;
   const int lane = threadIdx.x;
@@ -494,7 +506,17 @@ __global__ __launch_bounds__(64) LZ4R_WPE void lz4_tiles(
   uint64_t prof_last = 0;
 #endif
 
-  for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  // XCD-aware order: workgroups w and w + 8 share an XCD (observed round-robin
+  // dealing), so XCD w % 8 takes the contiguous slice [(w % 8) per, ...) of
+  // the blocks and a 128-B line shared by two neighbouring blocks is fetched
+  // into one L2, not two (a speed matter only: any mapping is correct).
+  const size_t per = (ntiles - t_first + 7) / 8;
+#ifndef LZ4R_XCD
+#define LZ4R_XCD 1
+#endif
+  const size_t t_mine = LZ4R_XCD ? t_first + (blockIdx.x & 7) * per + (blockIdx.x >> 3)
+                                 : t_first + blockIdx.x;
+  for (size_t t = t_mine; t < ntiles; t = ntiles) {   // one tile per workgroup
     const size_t b0 = t * kTB;
     const int nbt = (int)min((size_t)kTB, nb_total - b0);
     const size_t byte0 = b0 * kBlk;
@@ -560,12 +582,13 @@ constexpr int kPart = 64 * kGT;      // tiles per scan partial (64 groups)
 
 // per group of 64 tiles: gsum; per 64 groups: part
 __global__ __launch_bounds__(256) void lz4_scan_reduce(const uint32_t *__restrict__ tsz,
-                                                       size_t ntiles,
+                                                       size_t ntiles, size_t p_first,
                                                        uint32_t *__restrict__ gsum,
                                                        uint64_t *__restrict__ part) {
   __shared__ uint64_t ws[4];
   const int tid = threadIdx.x;
-  const size_t t0 = (size_t)blockIdx.x * kPart + (size_t)tid * 16;   // 16 tiles per thread
+  const size_t pi = p_first + blockIdx.x;                            // partial index
+  const size_t t0 = pi * kPart + (size_t)tid * 16;                   // 16 tiles per thread
   uint32_t v = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -574,22 +597,25 @@ __global__ __launch_bounds__(256) void lz4_scan_reduce(const uint32_t *__restric
   }
   v += __shfl_xor(v, 1, 64);
   v += __shfl_xor(v, 2, 64);                      // 4 threads = one group of 64 tiles
-  const size_t g = (size_t)blockIdx.x * 64 + (tid >> 2);
+  const size_t g = pi * 64 + (tid >> 2);
   if ((tid & 3) == 0 && g * kGT < ntiles) gsum[g] = v;
   uint64_t w = (tid & 3) == 0 ? v : 0;
   w = wave_sum64(w);
   if ((tid & 63) == 0) ws[tid >> 6] = w;
   __syncthreads();
-  if (tid == 0) part[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+  if (tid == 0) part[pi] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// one workgroup: exclusive scan of the partials in place; total -> *len
+// one workgroup: exclusive scan of the partials in place, as absolute stream
+// offsets.  The scan starts at `hdr` (first != 0) or at *len (a continuation)
+// and leaves its end in *len.
 __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__ part,
                                                           size_t nparts, uint64_t hdr,
+                                                          int first,
                                                           uint64_t *__restrict__ len) {
   __shared__ uint64_t ws[16];
   __shared__ uint64_t carry;
-  if (threadIdx.x == 0) carry = 0;
+  if (threadIdx.x == 0) carry = first ? hdr : *len;
   __syncthreads();
   for (size_t c0 = 0; c0 < nparts; c0 += 1024) {
     const size_t i = c0 + threadIdx.x;
@@ -609,88 +635,96 @@ __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__
     if (threadIdx.x == 1023) carry = pre + x;
     __syncthreads();
   }
-  if (threadIdx.x == 0) *len = hdr + carry;
+  if (threadIdx.x == 0) *len = carry;
 }
 
-// 16 bytes starting at byte `off` of a slot (off may be -15 .. slot size;
-// slots are preceded by a 16-B pad, so the aligned loads stay in bounds)
-__device__ __forceinline__ uint4 load16(const uint8_t *slot, long off) {
-  const long a = off & ~15L;
-  const uint4 *q = reinterpret_cast<const uint4 *>(slot + a);
-  return funnel16(q[0], q[1], (int)(off - a));
-}
 
-__device__ __forceinline__ uint4 select16(uint4 x, uint4 y, int k) {
-  // bytes < k from x, the rest from y (0 <= k <= 16)
-  uint32_t xv[4] = {x.x, x.y, x.z, x.w}, yv[4] = {y.x, y.y, y.z, y.w}, o[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int lo = k - 4 * i;                     // bytes of this dword from x
-    const uint32_t m = lo <= 0 ? 0u : (lo >= 4 ? ~0u : ((1u << (8 * lo)) - 1u));
-    o[i] = (xv[i] & m) | (yv[i] & ~m);
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
-}
 
-// Workgroup = group of 64 consecutive tiles.  Offsets from the partials,
-// the group sums and a wave scan; then the group's output range is written
-// as aligned 16-B chunks, each assembled from at most two blocks' slots (a
-// full 300-B block encodes to >= 16 B: p = 0 is a literal, so it takes two
-// sequences, 3 + 7 + 6 bytes at the least; only the globally last is shorter).  Only the group's two edge
+// Workgroup = group of 64 consecutive blocks.  Offsets from the partials, the
+// group sums and a wave scan.  The group's bytes are assembled in LDS: each
+// slot's 16-B chunks are read with aligned, coalesced loads (the four waves
+// take 16 slots each, chunks flattened over the lanes) and written at the
+// slot's place in the output range (unaligned LDS stores; a slot's last chunk
+// writes its W % 16 bytes exactly, so slots never overwrite each other).
+// Then the range leaves as aligned 16-B stores; only the group's two edge
 // chunks are written bytewise.  Also writes the frame byte (LZ4.c:429).
+#ifndef LZ4R_GH
+#define LZ4R_GH 32
+#endif
+constexpr int kGH = LZ4R_GH;                         // blocks per gather workgroup
+constexpr int kGSplit = kGT / kGH;                   // workgroups per group
+constexpr int kGatherLds = kGH * kBlkOutMax + 32;    // worst case: every block 548 B
 __global__ __launch_bounds__(256) void lz4_gather(
     const uint8_t *__restrict__ slots, const uint32_t *__restrict__ tsz, size_t ntiles,
-    const uint32_t *__restrict__ gsum, const uint64_t *__restrict__ part,
+    size_t g_first, const uint32_t *__restrict__ gsum, const uint64_t *__restrict__ part,
     uint8_t *__restrict__ out, uint64_t cap, int hdr, uint64_t nb_total) {
   __shared__ uint64_t toff[kGT + 1];
-  const int tid = threadIdx.x;
-  const size_t g = blockIdx.x;
+  __shared__ uint32_t cex[kGT + 1];                  // exclusive chunk counts
+  __shared__ alignas(16) uint8_t img[kGatherLds];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const size_t g = g_first + blockIdx.x / kGSplit;
+  const int h0 = (int)(blockIdx.x % kGSplit) * kGH;  // this workgroup: blocks [h0, h0 + kGH)
   const size_t g0 = g * kGT;
   const int nt = (int)min((size_t)kGT, ntiles - g0);
+  if (h0 >= nt) return;
+  const int h1 = min(nt, h0 + kGH);
   if (tid < 64) {
     const size_t p = g0 / kPart;
     const size_t gfirst = p * 64;                  // first group of the partial
     uint64_t s = (gfirst + tid < g) ? gsum[gfirst + tid] : 0u;
     s = wave_sum64(s);
-    const uint64_t base = part[p] + s + (uint64_t)hdr;
+    const uint64_t base = part[p] + s;             // part[] holds absolute offsets
     const uint32_t v = tid < nt ? tsz[g0 + tid] : 0u;
     const uint32_t inc = wave_incl_add(v);
     toff[tid] = base + inc - v;
     if (tid == 63) toff[kGT] = base + inc;
+    const uint32_t ck = (tid >= h0 && tid < h1) ? (v + 15u) >> 4 : 0u;
+    const uint32_t cinc = wave_incl_add(ck);
+    cex[tid] = cinc - ck;
+    if (tid == 63) cex[kGT] = cinc;
   }
   __syncthreads();
-  if (hdr && g == 0 && tid == 0 && cap > 0) out[0] = (uint8_t)nb_total;
-  const uint64_t G0 = toff[0];
-  const uint64_t G1 = min(toff[nt], cap);
-  if (G1 <= G0) return;
-  const uintptr_t abs0 = (uintptr_t)(out + G0), absend = (uintptr_t)(out + G1);
-  const uintptr_t first = abs0 & ~(uintptr_t)15;
-  const long nchunks = (long)((absend - first + 15) >> 4);
-  // each wave takes a contiguous quarter of the chunks, 64 at a time, so a
-  // lane's block cursor moves ~3 blocks per step (a 256-chunk stride moved ~13)
-  const long per = ((nchunks + 255) >> 8) << 6;
-  const long c0 = (long)(tid >> 6) * per, c1 = min(nchunks, c0 + per);
-  int t = 0;                                       // block cursor (chunks ascend per lane)
-  if (c0 + (tid & 63) < c1) {                      // start: largest t with toff[t] <= first chunk
-    const uint64_t oa = (uint64_t)(first + ((uintptr_t)(c0 + (tid & 63)) << 4) - (uintptr_t)out);
-    int hi = nt - 1;
-    while (t < hi) {
-      const int mid = (t + hi + 1) >> 1;
-      if (toff[mid] <= oa) t = mid; else hi = mid - 1;
+  if (hdr && g == 0 && h0 == 0 && tid == 0 && cap > 0) out[0] = (uint8_t)nb_total;
+  const uint64_t G0 = toff[h0];
+  const uintptr_t abs0 = (uintptr_t)(out + G0);
+  const int lead = (int)(abs0 & 15);               // img[lead] = stream byte G0
+  // ---- slots -> LDS image -----------------------------------------------------
+  {
+    constexpr int kPer = kGH / 4;                  // slots per wave
+    const int s0 = h0 + wv * kPer, s1 = min(h1, s0 + kPer);
+    if (s0 < s1) {
+      const int c0 = (int)cex[s0], c1 = (int)cex[s1];
+      int t = s0;                                  // slot cursor (chunks ascend per lane)
+      for (int c = c0 + lane; c < c1; c += 64) {
+        while (t + 1 < s1 && (int)cex[t + 1] <= c) ++t;
+        const int j = c - (int)cex[t];
+        const uint4 v = reinterpret_cast<const uint4 *>(slots + (g0 + t) * (size_t)kSlot)[j];
+        uint8_t *d = img + lead + (int)(toff[t] - G0) + 16 * j;
+        const int m = (int)(toff[t + 1] - toff[t]) - 16 * j;   // bytes of this slot left
+        uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        const uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+        if (m >= 16) {
+          *reinterpret_cast<u64u *>(d) = lo;
+          *reinterpret_cast<u64u *>(d + 8) = hi;
+        } else {
+          if (m & 8) { *reinterpret_cast<u64u *>(d) = lo; d += 8; lo = hi; }
+          if (m & 4) { *reinterpret_cast<u32u *>(d) = (uint32_t)lo; d += 4; lo >>= 32; }
+          if (m & 2) { *reinterpret_cast<u16u *>(d) = (uint16_t)lo; d += 2; lo >>= 16; }
+          if (m & 1) *d = (uint8_t)lo;
+        }
+      }
     }
   }
-  for (long ci = c0 + (tid & 63); ci < c1; ci += 64) {
+  __syncthreads();
+  // ---- LDS image -> stream (aligned 16-B stores) --------------------------------
+  const uint64_t G1 = min(toff[h1], cap);
+  if (G1 <= G0) return;
+  const uintptr_t absend = (uintptr_t)(out + G1);
+  const uintptr_t first = abs0 & ~(uintptr_t)15;
+  const int nchunks = (int)((absend - first + 15) >> 4);
+  for (int ci = tid; ci < nchunks; ci += 256) {
     const uintptr_t a = first + ((uintptr_t)ci << 4);
-    const uint64_t oa = (uint64_t)(a - (uintptr_t)out);   // stream offset of the chunk
-    const uint64_t ob = oa < G0 ? G0 : oa;
-    while (t + 1 < nt && toff[t + 1] <= ob) ++t;
-    const uint8_t *s0 = slots + (g0 + t) * (size_t)kSlot;
-    uint4 v = load16(s0, (long)oa - (long)toff[t]);
-    const uint64_t nx = toff[t + 1];               // next tile's first byte
-    if (t + 1 < nt && nx < oa + 16) {
-      const uint8_t *s1 = slots + (g0 + t + 1) * (size_t)kSlot;
-      v = select16(v, load16(s1, (long)oa - (long)nx), (int)(nx - oa));
-    }
+    const uint4 v = reinterpret_cast<const uint4 *>(img)[ci];
     if (a >= abs0 && a + 16 <= absend) {
       *reinterpret_cast<uint4 *>(a) = v;
     } else {
@@ -770,29 +804,34 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   const size_t nb = (n + kBlk - 1) / kBlk;
   int rc = ensure_scratch(c, nb);
   if (rc != LZ4R_OK) return rc;
-  const size_t ntiles = (nb + kTB - 1) / kTB;
   if (nb > 0xffffffffULL || n > (1ull << 37)) return LZ4R_ERR_ARG;
+  static_assert(kTB == 1 && kPart % kGT == 0, "tiles are blocks; partials hold whole groups");
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool timed = c->timing;
   c->timed_call = timed;
   if (timed) (void)hipEventRecord(c->ev_a, s);
   // one tile per workgroup: the hardware dispatcher balances the uneven
-  // per-tile cost (a static grid-stride split leaves a tail)
-  hipLaunchKernelGGL(lz4_tiles, dim3((unsigned)ntiles), dim3(64), 0, s,
-                     static_cast<const uint8_t *>(d_in), n, nb, ntiles, c->slots, c->tsz,
+  // per-tile cost (a static grid-stride split leaves a tail; measured slower
+  // also with the next block prefetched into registers)
+  hipLaunchKernelGGL(lz4_tiles, dim3((unsigned)(8 * ((nb + 7) / 8))), dim3(64), 0, s,
+                     static_cast<const uint8_t *>(d_in), n, nb, (size_t)0, nb, c->slots, c->tsz,
                      c->bsizes);
   if (timed) (void)hipEventRecord(c->ev_b, s);
   const size_t nparts = (nb + kPart - 1) / kPart;
   hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)nparts), dim3(256), 0, s, c->tsz, nb,
-                     c->gsum, c->part);
+                     (size_t)0, c->gsum, c->part);
   hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part, nparts,
-                     (uint64_t)hdr, static_cast<uint64_t *>(d_len));
-  hipLaunchKernelGGL(lz4_gather, dim3((unsigned)((nb + kGT - 1) / kGT)), dim3(256), 0, s,
-                     c->slots, c->tsz, nb, c->gsum, c->part,
-                     static_cast<uint8_t *>(d_out), (uint64_t)cap, hdr, (uint64_t)nb);
+                     (uint64_t)hdr, 1, static_cast<uint64_t *>(d_len));
+  const size_t ngroups = (nb + kGT - 1) / kGT;
+  hipLaunchKernelGGL(lz4_gather, dim3((unsigned)(ngroups * kGSplit)), dim3(256), 0, s, c->slots,
+                     c->tsz, nb, (size_t)0, c->gsum, c->part, static_cast<uint8_t *>(d_out),
+                     (uint64_t)cap, hdr, (uint64_t)nb);
   if (timed) (void)hipEventRecord(c->ev_c, s);
   c->last_nb = nb;
-  return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess && getenv("LZ4R_DEBUG"))
+    fprintf(stderr, "lz4r: %s\n", hipGetErrorString(e));
+  return e == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
 }
 
 }  // namespace
@@ -858,9 +897,12 @@ int lz4r_compress_device(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, s
   if (rc != LZ4R_OK) return rc;
   uint64_t need = 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipMemcpyAsync(&need, c->len, sizeof(need), hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
+  hipError_t e = hipMemcpyAsync(&need, c->len, sizeof(need), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    if (getenv("LZ4R_DEBUG")) fprintf(stderr, "lz4r: %s\n", hipGetErrorString(e));
     return LZ4R_ERR_HIP;
+  }
   *out_len = (size_t)need;
   return need > cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
 }
