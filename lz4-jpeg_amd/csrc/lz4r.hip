@@ -94,11 +94,8 @@ constexpr int kBlkOutMax = 560;           // >= 548: worst-case bytes of one blo
 // kBlkOutMax); the tile's input sits at kInOff + 300k; then an over-read pad.
 constexpr int kInOff = kBlkOutMax;
 constexpr int kRegion = kInOff + kTileIn + 48;  // + over-read pad (lcp, 32-B copy reads)
-#ifndef LZ4R_HEAD16
-#define LZ4R_HEAD16 1
-#endif
 #ifndef LZ4R_HB
-#define LZ4R_HB (LZ4R_HEAD16 ? 9 : 8)
+#define LZ4R_HB 9
 #endif
 constexpr int kHB = LZ4R_HB;              // hash bits: 512 buckets
 constexpr int kH = 1 << kHB;
@@ -114,11 +111,7 @@ static_assert(kSlot % 16 == 0 && kBlkOutMax / 16 <= 64, "aligned slots, one stor
 struct TileLds {
   alignas(16) uint8_t buf[kRegion];
   union {
-#if LZ4R_HEAD16
     uint32_t head[kH / 2];  // bucket -> 1 + last inserted position (0: empty), u16 pairs
-#else
-    uint32_t head[kH];    // bucket -> 1 + last inserted position (0: empty)
-#endif
     uint32_t q[kQ];       // then: chain walkers, walker | next chain entry << 16
     uint32_t seq[kArr];   // then: per sequence, cpos | end << 16
   };
@@ -131,21 +124,30 @@ struct TileLds {
 };
 
 
-__device__ __forceinline__ uint32_t load4u(const uint8_t *b, int off) {
-  const uint32_t *d = reinterpret_cast<const uint32_t *>(b);
-  const uint32_t w0 = d[off >> 2], w1 = d[(off >> 2) + 1];
-  return __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(off & 3));
+
+__device__ __forceinline__ uint32_t lds_off(const uint32_t *a) {
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  return (uint32_t)(uintptr_t)(lds_u32 *)a;
 }
 
-// ds_mskor_rtn_b32: *a = (*a & ~clear) | set, returns the old dword (one LDS
-// atomic: a 16-bit exchange inside a dword of two bucket heads)
-__device__ __forceinline__ uint32_t mskor_rtn(uint32_t *a, uint32_t clear, uint32_t set) {
-  typedef __attribute__((address_space(3))) uint32_t lds_u32;
-  const uint32_t off = (uint32_t)(uintptr_t)(lds_u32 *)a;
-  uint32_t old;
-  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
-               : "=v"(old) : "v"(off), "v"(clear), "v"(set) : "memory");
-  return old;
+// Five ds_mskor_rtn_b32 back to back, one wait: *a = (*a & ~clear) | set,
+// returning the old dword -- a 16-bit exchange inside a dword of two bucket
+// heads (no 16-bit LDS exchange exists).  The LDS serves one wave's
+// operations in order, so a later swap of the same head sees the earlier.
+__device__ __forceinline__ void mskor_rtn5(uint32_t (&old)[5], const uint32_t (&a)[5],
+                                           const uint32_t (&clr)[5], const uint32_t (&set)[5]) {
+  asm volatile(
+      "ds_mskor_rtn_b32 %0, %5, %10, %15\n\t"
+      "ds_mskor_rtn_b32 %1, %6, %11, %16\n\t"
+      "ds_mskor_rtn_b32 %2, %7, %12, %17\n\t"
+      "ds_mskor_rtn_b32 %3, %8, %13, %18\n\t"
+      "ds_mskor_rtn_b32 %4, %9, %14, %19\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(old[0]), "=&v"(old[1]), "=&v"(old[2]), "=&v"(old[3]), "=&v"(old[4])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]),
+        "v"(clr[0]), "v"(clr[1]), "v"(clr[2]), "v"(clr[3]), "v"(clr[4]),
+        "v"(set[0]), "v"(set[1]), "v"(set[2]), "v"(set[3]), "v"(set[4])
+      : "memory");
 }
 
 typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned LDS access (the LDS
@@ -255,30 +257,56 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
   // pass over the queue is balanced over the lanes whatever the chain lengths.
   const bool search = LZ4R_VARIANT != 1 && LZ4R_VARIANT != 2;
   const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
-  constexpr int kHeadW = LZ4R_HEAD16 ? kH / 2 : kH;   // head dwords
+  constexpr int kHeadW = kH / 2;          // head dwords (u16 heads)
   static_assert(kHeadW % 256 == 0, "head reset: 16-B stores");
 #pragma unroll
   for (int i = 0; i < kHeadW / 256; ++i)  // empty heads (the previous block's queue)
     reinterpret_cast<uint4 *>(S.head)[i * 64 + lane] = make_uint4(0, 0, 0, 0);
+  // Blocked layout: lane l owns the five positions p0 .. p0 + 4, p0 = 5 l
+  // (lanes 60..63 own none of a 300-B block).  One 12-byte window per lane
+  // gives all five 4-gram keys and preceding bytes; the five head swaps go
+  // out back to back.  Chain order need not follow position order: a pair is
+  // met once whichever of the two was inserted later, and is ordered by
+  // position when it is used.
+  const int p0 = 5 * lane;
   uint32_t item[5];
+  {
+    // bytes p0 - 1 .. p0 + 10 (lane 0's byte -1 unused) from four aligned dwords
+    const int wb = base + p0 - 1;
+    const uint32_t *wd = reinterpret_cast<const uint32_t *>(S.buf) + (wb >> 2);
+    const uint32_t a0 = wd[0], a1 = wd[1], a2 = wd[2], a3 = wd[3];
+    const uint32_t wsh = (uint32_t)(wb & 3);
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(a1, a0, wsh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(a2, a1, wsh);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(a3, a2, wsh);
+    const uint32_t key[5] = {__builtin_amdgcn_alignbyte(d1, d0, 1u),
+                             __builtin_amdgcn_alignbyte(d1, d0, 2u),
+                             __builtin_amdgcn_alignbyte(d1, d0, 3u), d1,
+                             __builtin_amdgcn_alignbyte(d2, d1, 1u)};
+    uint32_t adr[5], clr[5], set[5], sh[5], tg[5];
 #pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int p = r * 64 + lane;
-    if (p < n) S.rec[p] = 0u;            // local(p) accumulator
-    item[r] = 0u;
-    if (search && p < nk) {
-      const uint32_t key = load4u(S.buf, base + p);
-      const uint32_t pb = p >= 1 ? (uint32_t)S.buf[base + p - 1] : 0u;
-      const uint32_t tag = (key * 2654435761u) >> 17;
-#if LZ4R_HEAD16
-      const uint32_t bk = tag >> (15 - kHB), sh = (bk & 1u) << 4;
-      const uint32_t old = mskor_rtn(&S.head[bk >> 1], 0xFFFFu << sh, ((uint32_t)p + 1u) << sh) >> sh & 0xFFFFu;
-#else
-      const uint32_t old = atomicExch(&S.head[tag >> (15 - kHB)], (uint32_t)p + 1u);
-#endif
-      const uint32_t link = old ? old - 1u : 511u;
-      S.ent[p] = link | (pb << 9) | (tag << 17);
-      item[r] = old ? (uint32_t)p | (link << 16) : 0u;
+    for (int r = 0; r < 5; ++r) {
+      const int p = p0 + r;
+      if (p < n) S.rec[p] = 0u;                          // local(p) accumulator
+      const bool act = search && p < nk;
+      tg[r] = (key[r] * 2654435761u) >> 17;
+      const uint32_t bk = tg[r] >> (15 - kHB);
+      sh[r] = (bk & 1u) << 4;
+      adr[r] = lds_off(act ? &S.head[bk >> 1] : &S.cand[lane]);   // inactive: own dword
+      clr[r] = act ? 0xFFFFu << sh[r] : 0u;               // inactive: a no-op swap
+      set[r] = act ? ((uint32_t)p + 1u) << sh[r] : 0u;
+    }
+    uint32_t old[5];
+    mskor_rtn5(old, adr, clr, set);
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int p = p0 + r;
+      const uint32_t o = (old[r] >> sh[r]) & 0xFFFFu;
+      const uint32_t link = o ? o - 1u : 511u;
+      const uint32_t pb = r < 4 ? (d0 >> (8 * r)) & 255u : d1 & 255u;   // blk[p - 1]
+      const bool act = search && p < nk;
+      if (act) S.ent[p] = link | (pb << 9) | (tg[r] << 17);
+      item[r] = act && o ? (uint32_t)p | (link << 16) : 0u;
     }
   }
   __syncthreads();                       // the heads are dead: the queue overlays them
@@ -354,56 +382,61 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
   PROF_T(1);
   __syncthreads();
   PROF_T(2);
-  int bl[5], bj[5];
-#pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int p = r * 64 + lane;
-    const uint32_t v = p < n ? S.rec[p] : 0u;
-    bl[r] = (int)(v >> 9);
-    bj[r] = 511 - (int)(v & 511u);
-  }
-
   // ---- best(p) = prefix lexmax of (end, dist) -------------------------------
-  uint32_t mrec[5];
-  uint64_t mask[5];
-  uint32_t carry = 0;
+  // blocked: a running max over the lane's five positions, one wave scan of
+  // the lane totals, the exclusive prefix folded back in
+  uint32_t v[5];
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
-    const int p = r * 64 + lane;
-    uint32_t v = bl[r] >= 4 ? (((uint32_t)(p + bl[r]) << 9) | (uint32_t)(p - bj[r])) : 0u;
-    v = max(wave_incl_max(v), carry);
-    carry = lane63(v);
-    const int len = (int)(v >> 9) - p;                  // >= 4 iff a match starts here
+    const int p = p0 + r;
+    const uint32_t rv = p < n ? S.rec[p] : 0u;
+    const int bl = (int)(rv >> 9), bj = 511 - (int)(rv & 511u);
+    v[r] = bl >= 4 ? (((uint32_t)(p + bl) << 9) | (uint32_t)(p - bj)) : 0u;
+    if (r) v[r] = max(v[r], v[r - 1]);
+  }
+  {
+    const uint32_t incl = wave_incl_max(v[4]);
+    const uint32_t excl = dpp<0x138, 0xf, 0xf>(incl);     // wave_shr:1, lane 0 gets 0
+#pragma unroll
+    for (int r = 0; r < 5; ++r) v[r] = max(v[r], excl);
+  }
+  uint32_t mrec[5];
+  int f[6];                       // f[r] = first matchable position >= p0 + r
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int len = (int)(v[r] >> 9) - (p0 + r);        // >= 4 iff a match starts here
     const int M = len >= 4 ? (len & 255) : 0;           // uint8_t return, LZ4.c:317
-    mrec[r] = (uint32_t)M | ((v & 511u) << 8);
-    mask[r] = __ballot(M != 0);
+    mrec[r] = (uint32_t)M | ((v[r] & 511u) << 8);
   }
 
   // ---- nm(x): first matchable position >= x, for x in [0, n] ---------------
-  int F[6];
-  F[5] = n;
+  {
+    int loc = 1 << 20;            // the lane's own first matchable position
 #pragma unroll
-  for (int r = 4; r >= 0; --r) F[r] = mask[r] ? r * 64 + ctz64(mask[r]) : F[r + 1];
+    for (int r = 4; r >= 0; --r) loc = (mrec[r] & 255u) ? p0 + r : loc;
+    const uint64_t has = __ballot(loc < (1 << 20));
+    const uint64_t up = has & ~((2ull << lane) - 1ull);  // lanes above this one
+    const int src = up ? ctz64(up) : lane;
+    const int nx = __shfl(loc, src, 64);
+    f[5] = up ? nx : n;
 #pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int p = r * 64 + lane;
-    if (p <= n) {
-      const uint64_t m = mask[r] & (~0ull << lane);
-      S.nm[p] = (uint16_t)(m ? r * 64 + ctz64(m) : F[r + 1]);
-    }
+    for (int r = 4; r >= 0; --r) f[r] = (mrec[r] & 255u) ? p0 + r : f[r + 1];
+#pragma unroll
+    for (int r = 0; r < 5; ++r)
+      if (p0 + r <= n) S.nm[p0 + r] = (uint16_t)f[r];
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
-    const int p = r * 64 + lane;
     const int M = (int)(mrec[r] & 255u);
-    if (M != 0) S.rec[p] = mrec[r] | ((uint32_t)S.nm[p + M] << 17);
+    if (M != 0) S.rec[p0 + r] = mrec[r] | ((uint32_t)S.nm[p0 + r + M] << 17);
   }
+  const int F0 = __builtin_amdgcn_readlane(f[0], 0);    // nm(0)
   __syncthreads();
 
   PROF_T(3);
   // ---- greedy parse = walk over match starts (LZ4.c:516-583) ---------------
-  int c = F[0], e = 0, Sv = 0;
+  int c = F0, e = 0, Sv = 0;
   while (c < n) {
     const uint32_t rv = __builtin_amdgcn_readfirstlane(S.rec[c]);
     e = c + (int)(rv & 255u);
