@@ -237,6 +237,16 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 
 
 
+// The compressor's workgroup is one wave.  A wave's LDS operations are
+// served in order, so its phase boundaries need neither s_barrier nor the
+// s_waitcnt vmcnt(0) lgkmcnt(0) that __syncthreads() implies: a compiler
+// barrier that keeps the LDS accesses of both phases in program order is
+// enough, and loads still in flight (LDS or global) stay in flight.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Encode block `k` of the tile (n bytes at S.buf[kInOff + 300k]) into
 // S.buf[obase ...]; returns the bytes written.
 __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
@@ -309,7 +319,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
       item[r] = act && o ? (uint32_t)p | (link << 16) : 0u;
     }
   }
-  __syncthreads();                       // the heads are dead: the queue overlays them
+  wave_sync();                       // the heads are dead: the queue overlays them
   int qwr = 0;                           // walkers queued (S.q[0 .. qwr))
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
@@ -318,7 +328,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     if (walk) S.q[qwr + __popcll(wm & lanemask_lt())] = item[r];
     qwr += __popcll(wm);
   }
-  __syncthreads();
+  wave_sync();
 
   PROF_T(0);
   // ---- candidates: walk the chains ------------------------------------------
@@ -330,14 +340,14 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     constexpr int kTrash = kCand - 1;
     int ncand = 0;
     auto drain = [&]() {
-      __syncthreads();
+      wave_sync();
       for (int i = lane; i < ncand && LZ4R_VARIANT != 4; i += 64) {
         const uint32_t pr = S.cand[i];
         const int p = (int)(pr & 0xFFFFu), j = (int)(pr >> 16);
         const int l = lcp(S.buf, base + j, base + p, n - p);
         if (l >= 4) atomicMax(&S.rec[p], ((uint32_t)l << 9) | (uint32_t)(511 - j));
       }
-      __syncthreads();
+      wave_sync();
     };
     // ring of walkers: a pass reads up to 64, then queues those that go on
     // (at most one walker per entry is ever live: <= kQ)
@@ -380,7 +390,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     if (ncand) drain();
   }
   PROF_T(1);
-  __syncthreads();
+  wave_sync();
   PROF_T(2);
   // ---- best(p) = prefix lexmax of (end, dist) -------------------------------
   // blocked: a running max over the lane's five positions, one wave scan of
@@ -425,26 +435,29 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     for (int r = 0; r < 5; ++r)
       if (p0 + r <= n) S.nm[p0 + r] = (uint16_t)f[r];
   }
-  __syncthreads();
+  wave_sync();
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     const int M = (int)(mrec[r] & 255u);
     if (M != 0) S.rec[p0 + r] = mrec[r] | ((uint32_t)S.nm[p0 + r + M] << 17);
   }
   const int F0 = __builtin_amdgcn_readlane(f[0], 0);    // nm(0)
-  __syncthreads();
+  wave_sync();
 
   PROF_T(3);
   // ---- greedy parse = walk over match starts (LZ4.c:516-583) ---------------
+  // (v_readlane of the owning lane's registers instead of the LDS read was
+  // measured 25 % slower: readlane stalls the SIMD's VALU pipeline)
   int c = F0, e = 0, Sv = 0;
-  while (c < n) {
+  while (c < n) {          // succ(c) > c: at most n steps (a hard bound)
     const uint32_t rv = __builtin_amdgcn_readfirstlane(S.rec[c]);
     e = c + (int)(rv & 255u);
-    if (lane == 0) S.seq[Sv] = (uint32_t)c | ((uint32_t)e << 16);
+    // sequence entry: cpos | M << 9 | dist << 17 (the emission needs no rec read)
+    if (lane == 0) S.seq[Sv] = (uint32_t)c | ((rv & 0x1FFFFu) << 9);
     ++Sv;
     c = (int)(rv >> 17);
   }
-  __syncthreads();
+  wave_sync();
   PROF_T(4);
   // ---- sequences: lane kk = sequence kk ------------------------------------
   const int nseq = Sv + (e < n ? 1 : 0);
@@ -457,11 +470,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     int M = 0, D = 0, cpos = n, end = n;
     if (act && kk < Sv) {
       const uint32_t sq = S.seq[kk];
-      cpos = (int)(sq & 0xFFFFu);
-      end = (int)(sq >> 16);
-      const uint32_t rv = S.rec[cpos];
-      M = (int)(rv & 255u);
-      D = (int)((rv >> 8) & 511u);
+      cpos = (int)(sq & 511u);
+      M = (int)((sq >> 9) & 255u);
+      D = (int)(sq >> 17);
+      end = cpos + M;
     }
     const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
     const int pend = lane == 0 ? end_prev : (int)upv;             // literal run start
@@ -521,7 +533,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     S.buf[obase + 1] = (uint8_t)(bsz & 255);
     S.buf[obase + 2] = (uint8_t)((bsz >> 8) & 255);
   }
-  __syncthreads();
+  wave_sync();
   PROF_T(5);
   return ocar;
 }
@@ -581,7 +593,7 @@ __global__ __launch_bounds__(64) LZ4R_WPE void lz4_tiles(
       for (int i = done + lane; i < len; i += 64) dst[i] = src[i];
       if (lane < 16) dst[len + lane] = 0;
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- encode the tile's blocks; each leaves for its slot at once ---------
     for (int k = 0; k < nbt; ++k) {
@@ -600,7 +612,7 @@ __global__ __launch_bounds__(64) LZ4R_WPE void lz4_tiles(
       }
       PROF_T(9);
     }
-    __syncthreads();                                // LDS reused by the next tile
+    wave_sync();                                // LDS reused by the next tile
     PROF_T(9);
   }
 #ifdef LZ4R_PROF
@@ -846,7 +858,8 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   // one tile per workgroup: the hardware dispatcher balances the uneven
   // per-tile cost (a static grid-stride split leaves a tail; measured slower
   // also with the next block prefetched into registers)
-  hipLaunchKernelGGL(lz4_tiles, dim3((unsigned)(8 * ((nb + 7) / 8))), dim3(64), 0, s,
+  static const unsigned extra_lds = getenv("LZ4R_EXTRA_LDS") ? (unsigned)atoi(getenv("LZ4R_EXTRA_LDS")) : 0u;
+  hipLaunchKernelGGL(lz4_tiles, dim3((unsigned)(8 * ((nb + 7) / 8))), dim3(64), extra_lds, s,
                      static_cast<const uint8_t *>(d_in), n, nb, (size_t)0, nb, c->slots, c->tsz,
                      c->bsizes);
   if (timed) (void)hipEventRecord(c->ev_b, s);
