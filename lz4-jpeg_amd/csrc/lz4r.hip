@@ -118,6 +118,7 @@ struct TileLds {
   union {
     uint32_t ent[kArr];   // per position: link | preceding byte << 9 | tag << 17
     uint16_t nm[kArr];    // then: first matchable position >= x
+    uint32_t jt[kArr];    // then: succ, succ^2, succ^3 of a match start (9 bits each)
   };
   uint32_t rec[kArr];     // local(p) accumulator; then M | dist<<8 | succ<<17
   uint32_t cand[kCand];   // candidate pairs p | j << 16 awaiting the lcp pass
@@ -436,27 +437,82 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
       if (p0 + r <= n) S.nm[p0 + r] = (uint16_t)f[r];
   }
   wave_sync();
+  // succ(p) = nm(p + M(p)) for the match starts; succ(n) = n.  Then the
+  // jump table jt[p] = succ(p) | succ^2(p) << 9 | succ^3(p) << 18 (two
+  // position-parallel gathers), so the serial walk below advances three
+  // sequences per LDS round trip.
+  int j1[5];
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
+    // branch-free: entries of positions that start no match (p = n included:
+    // succ(n) = n) are written too; only their succ bits are ever read
     const int M = (int)(mrec[r] & 255u);
-    if (M != 0) S.rec[p0 + r] = mrec[r] | ((uint32_t)S.nm[p0 + r + M] << 17);
+    const int q = min(p0 + r, kArr - 1);
+    const int sj = (int)S.nm[min(q + M, kArr - 1)];
+    j1[r] = M != 0 ? sj : n;
+    S.rec[q] = mrec[r] | ((uint32_t)j1[r] << 17);
   }
   const int F0 = __builtin_amdgcn_readlane(f[0], 0);    // nm(0)
+  wave_sync();
+  {
+    int j2[5];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) j2[r] = (int)(S.rec[j1[r]] >> 17);
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int j3 = (int)(S.rec[j2[r]] >> 17);
+      S.jt[min(p0 + r, kArr - 1)] =
+          (uint32_t)j1[r] | ((uint32_t)j2[r] << 9) | ((uint32_t)j3 << 18);
+    }
+  }
   wave_sync();
 
   PROF_T(3);
   // ---- greedy parse = walk over match starts (LZ4.c:516-583) ---------------
-  // (v_readlane of the owning lane's registers instead of the LDS read was
-  // measured 25 % slower: readlane stalls the SIMD's VALU pipeline)
-  int c = F0, e = 0, Sv = 0;
-  while (c < n) {          // succ(c) > c: at most n steps (a hard bound)
-    const uint32_t rv = __builtin_amdgcn_readfirstlane(S.rec[c]);
-    e = c + (int)(rv & 255u);
-    // sequence entry: cpos | M << 9 | dist << 17 (the emission needs no rec read)
-    if (lane == 0) S.seq[Sv] = (uint32_t)c | ((rv & 0x1FFFFu) << 9);
-    ++Sv;
-    c = (int)(rv >> 17);
+  // The walk is the serial part of the block: from c0 = nm(0), each step
+  // reads the jump-table word of the last recorded start (three more starts)
+  // and keeps it in lane `it` of a register (v_writelane; reading registers
+  // with v_readlane instead of the LDS was measured 25 % slower, and every
+  // scalar instruction in this loop is paid ~25 times per block).
+  int c = F0, it = 0;
+  uint32_t seqv = 0;
+  while (c < n) {                        // c recorded: word it = succ .. succ^3 of c
+    const uint32_t t = __builtin_amdgcn_readfirstlane(S.jt[c]);
+    // lane select = it mod 64: past 64 words (> 193 sequences) lanes are
+    // overwritten and the walk is redone below
+    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
+                 : "+v"(seqv) : "s"(t), "s"(it) : "m0");
+    ++it;
+    c = (int)(t >> 18);
   }
+  // sequence list: S.seq[0] = c0, S.seq[1 + 3 i + f] = field f of word i
+  if (lane == 0) S.seq[0] = (uint32_t)F0;
+  int Sv = F0 < n ? 1 : 0, last = F0;    // starts recorded; the last one
+  if (it <= 64) {
+    if (lane < it) {
+      S.seq[1 + 3 * lane] = seqv & 511u;
+      S.seq[2 + 3 * lane] = (seqv >> 9) & 511u;
+      S.seq[3 + 3 * lane] = seqv >> 18;
+    }
+    if (it) {                            // only the last word can hold n's
+      const uint32_t tl = __builtin_amdgcn_readlane(seqv, it - 1);
+      const int a = (int)(tl & 511u), b = (int)((tl >> 9) & 511u), d = (int)(tl >> 18);
+      const int cprev = it >= 2 ? (int)(__builtin_amdgcn_readlane(seqv, it - 2) >> 18) : F0;
+      Sv += 3 * (it - 1) + (a < n) + (b < n) + (d < n);
+      last = d < n ? d : b < n ? b : a < n ? a : cprev;
+    }
+  } else {                               // rare (truncated matches): walk again into the LDS
+    for (c = F0; c < n;) {
+      const uint32_t t = __builtin_amdgcn_readfirstlane(S.jt[c]);
+      const int a = (int)(t & 511u), b = (int)((t >> 9) & 511u), d = (int)(t >> 18);
+      if (lane >= 1 && lane <= 3) S.seq[Sv + lane - 1] = lane == 1 ? a : lane == 2 ? b : d;
+      Sv += (a < n) + (b < n) + (d < n);
+      last = d < n ? d : b < n ? b : a < n ? a : last;
+      c = d;
+    }
+  }
+  int e = 0;                             // end of the last match
+  if (Sv) e = last + (int)(__builtin_amdgcn_readfirstlane(S.rec[last]) & 255u);
   wave_sync();
   PROF_T(4);
   // ---- sequences: lane kk = sequence kk ------------------------------------
@@ -469,10 +525,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     const bool act = kk < nseq;
     int M = 0, D = 0, cpos = n, end = n;
     if (act && kk < Sv) {
-      const uint32_t sq = S.seq[kk];
-      cpos = (int)(sq & 511u);
-      M = (int)((sq >> 9) & 255u);
-      D = (int)(sq >> 17);
+      cpos = (int)S.seq[kk];
+      const uint32_t rv = S.rec[cpos];
+      M = (int)(rv & 255u);
+      D = (int)((rv >> 8) & 511u);
       end = cpos + M;
     }
     const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
