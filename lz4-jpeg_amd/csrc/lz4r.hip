@@ -161,18 +161,17 @@ typedef uint16_t u16u __attribute__((aligned(1)));
 // reads past the region land in its pad (>= 16 B past any block end).
 __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
   int l = 0;
-  while (l < limit) {                     // 16 bytes per step: half the loop overhead
+  bool diff;
+  do {                                    // 16 bytes per step, one exit condition
     const uint64_t x0 = *reinterpret_cast<const u64u *>(d + a + l) ^
                         *reinterpret_cast<const u64u *>(d + b + l);
     const uint64_t x1 = *reinterpret_cast<const u64u *>(d + a + l + 8) ^
                         *reinterpret_cast<const u64u *>(d + b + l + 8);
-    if (x0 | x1) {
-      l += x0 ? (__builtin_ctzll(x0) >> 3) : 8 + (__builtin_ctzll(x1) >> 3);
-      return l < limit ? l : limit;
-    }
-    l += 16;
-  }
-  return limit;
+    diff = (x0 | x1) != 0;
+    const int at = x0 ? (__builtin_ctzll(x0) >> 3) : 8 + (__builtin_ctzll(x1 | (1ull << 63)) >> 3);
+    l += diff ? at : 16;
+  } while (!diff && l < limit);
+  return l < limit ? l : limit;
 }
 
 // litext bytes (LZ4.c:548-560 accounting == 372-386 writing)
@@ -231,10 +230,16 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 
 __device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
 
-__device__ __forceinline__ uint64_t lanemask_lt() {
-  const int lane = threadIdx.x & 63;
-  return (1ull << lane) - 1ull;
+// lane mask of a predicate, straight from the compare (hip's __ballot goes
+// through a 0/1 VGPR and a second compare)
+__device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
+// set bits of m in the lanes below this one (v_mbcnt_lo / v_mbcnt_hi)
+__device__ __forceinline__ int rank_below(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
+
 
 
 
@@ -298,7 +303,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = p0 + r;
-      if (p < n) S.rec[p] = 0u;                          // local(p) accumulator
+      S.rec[min(p, kArr - 1)] = 0u;     // local(p) accumulator (branch-free: past n unused)
       const bool act = search && p < nk;
       tg[r] = (key[r] * 2654435761u) >> 17;
       const uint32_t bk = tg[r] >> (15 - kHB);
@@ -316,7 +321,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
       const uint32_t link = o ? o - 1u : 511u;
       const uint32_t pb = r < 4 ? (d0 >> (8 * r)) & 255u : d1 & 255u;   // blk[p - 1]
       const bool act = search && p < nk;
-      if (act) S.ent[p] = link | (pb << 9) | (tg[r] << 17);
+      S.ent[min(p, kArr - 1)] = link | (pb << 9) | (tg[r] << 17);   // inactive: never read
       item[r] = act && o ? (uint32_t)p | (link << 16) : 0u;
     }
   }
@@ -325,8 +330,9 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     const bool walk = item[r] != 0u;     // p != link, so a walker's item is never 0
-    const uint64_t wm = __ballot(walk);
-    if (walk) S.q[qwr + __popcll(wm & lanemask_lt())] = item[r];
+    const uint64_t wm = ballot(walk);
+    // branch-free: lanes without a walker write their own dword of the idle cand list
+    *(walk ? &S.q[qwr + rank_below(wm)] : &S.cand[lane]) = item[r];
     qwr += __popcll(wm);
   }
   wave_sync();
@@ -365,15 +371,15 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
       const uint32_t x = me ^ o;
       const int p = max(a, b), j = min(a, b);
       const bool cand = act && (x >> 17) == 0 && (j == 0 || (x & (255u << 9)) != 0);
-      const uint64_t cm = __ballot(cand);
-      const int sl = cand ? ncand + __popcll(cm & lanemask_lt()) : kTrash;
+      const uint64_t cm = ballot(cand);
+      const int sl = cand ? ncand + rank_below(cm) : kTrash;
       S.cand[sl] = (uint32_t)p | ((uint32_t)j << 16);
       ncand += __popcll(cm);
       const uint32_t nx = o & 511u;
       const bool go = act && nx != 511u;
-      const uint64_t gm = __ballot(go);
+      const uint64_t gm = ballot(go);
       if (go) {
-        int wi = qwr + __popcll(gm & lanemask_lt());
+        int wi = qwr + rank_below(gm);
         wi -= wi >= kQ ? kQ : 0;
         S.q[wi] = (uint32_t)a | (nx << 16);
       }
@@ -425,7 +431,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     int loc = 1 << 20;            // the lane's own first matchable position
 #pragma unroll
     for (int r = 4; r >= 0; --r) loc = (mrec[r] & 255u) ? p0 + r : loc;
-    const uint64_t has = __ballot(loc < (1 << 20));
+    const uint64_t has = ballot(loc < (1 << 20));
     const uint64_t up = has & ~((2ull << lane) - 1ull);  // lanes above this one
     const int src = up ? ctz64(up) : lane;
     const int nx = __shfl(loc, src, 64);
@@ -434,7 +440,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     for (int r = 4; r >= 0; --r) f[r] = (mrec[r] & 255u) ? p0 + r : f[r + 1];
 #pragma unroll
     for (int r = 0; r < 5; ++r)
-      if (p0 + r <= n) S.nm[p0 + r] = (uint16_t)f[r];
+      S.nm[min(p0 + r, kArr - 1)] = (uint16_t)f[r];   // past n: unused
   }
   wave_sync();
   // succ(p) = nm(p + M(p)) for the match starts; succ(n) = n.  Then the
@@ -481,7 +487,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     // lane select = it mod 64: past 64 words (> 193 sequences) lanes are
     // overwritten and the walk is redone below
     asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
-                 : "+v"(seqv) : "s"(t), "s"(it) : "m0");
+                 : "+v"(seqv) : "s"(t), "s"(it));   // m0: not used by this kernel otherwise
     ++it;
     c = (int)(t >> 18);
   }
