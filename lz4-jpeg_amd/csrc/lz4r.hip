@@ -174,24 +174,6 @@ __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
   return l < limit ? l : limit;
 }
 
-// litext bytes (LZ4.c:548-560 accounting == 372-386 writing)
-__device__ __forceinline__ int litext_len(int L) {
-  if (L < 15) return 0;
-  return ((L - 15) & 255) == 255 ? 2 : 1;
-}
-
-// bytes write_sequence emits for (L, M); M == 0 marks the literal-only tail
-__device__ __forceinline__ int seq_written(int L, int M) {
-  const int mext = (M >= 4 && ((M - 4) & 255) >= 15) ? 1 : 0;   // LZ4.c:393-411
-  return 3 + litext_len(L) + L + 2 + mext;
-}
-
-// byte_size the reference stores in the sequence (LZ4.c:546-575, :597-610)
-__device__ __forceinline__ int seq_size_field(int L, int M) {
-  const int mext = (M != 0 && ((M - 4) & 255) >= 15) ? 1 : 0;
-  return L + 5 + litext_len(L) + mext;
-}
-
 // DPP helpers (gfx9 row_shr / row_bcast; identity 0 for lanes without a source)
 template <int CTRL, int ROW, int BANK>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -529,37 +511,42 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
   for (int s0 = 0; s0 < nseq && LZ4R_VARIANT != 11; s0 += 64) {
     const int kk = s0 + lane;
     const bool act = kk < nseq;
-    int M = 0, D = 0, cpos = n, end = n;
-    if (act && kk < Sv) {
-      cpos = (int)S.seq[kk];
-      const uint32_t rv = S.rec[cpos];
-      M = (int)(rv & 255u);
-      D = (int)((rv >> 8) & 511u);
-      end = cpos + M;
-    }
+    const bool ism = kk < Sv;                                      // ends with a match
+    // branch-free reads: entries past Sv are garbage, clamped and discarded
+    const uint32_t cq = min(S.seq[min(kk, kArr - 1)], (uint32_t)(kArr - 1));
+    const uint32_t rv = S.rec[cq];
+    const int cpos = ism ? (int)cq : n;
+    const int M = ism ? (int)(rv & 255u) : 0;
+    const int D = ism ? (int)((rv >> 8) & 511u) : 0;             // the tail writes offset 0
+    const int end = cpos + M;
     const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
     const int pend = lane == 0 ? end_prev : (int)upv;             // literal run start
     end_prev = (int)lane63((uint32_t)end);
     const int L = cpos - pend;
-    const int W = act ? seq_written(L, M) : 0;
-    const int SZ = act ? seq_size_field(L, M) : 0;
-    const uint32_t inc = wave_incl_add((uint32_t)W | ((uint32_t)SZ << 16));
+    // bytes written (LZ4.c:365-413) and the size field (LZ4.c:546-575), which
+    // differ for M = 1..3: the field counts a match-extension byte that
+    // write_sequence never writes
+    const int rem = (L - 15) & 255;
+    const int le = L >= 15 ? (rem == 255 ? 2 : 1) : 0;             // literal-extension bytes
+    const int mx = (M - 4) & 255;
+    const bool mextW = M >= 4 && mx >= 15, mextS = M != 0 && mx >= 15;
+    const uint32_t ws = act ? (uint32_t)(5 + le + L) * 0x10001u + (mextW ? 1u : 0u) +
+                                  (mextS ? 0x10000u : 0u)
+                            : 0u;
+    const uint32_t inc = wave_incl_add(ws);
     const uint32_t tot = lane63(inc);
-    const int excl = (int)(inc & 0xFFFFu) - W;
+    const int excl = (int)((inc - ws) & 0xFFFFu);
     if (act) {
       int o = obase + ocar + excl;
       const int tl = L >= 15 ? 15 : L;                                // LZ4.c:540
-      const int tm = M == 0 ? 0 : (M >= 19 ? 15 : ((M - 4) & 255));   // LZ4.c:542
-      // token, u16 size, literal-extension bytes (LZ4.c:367-386) assembled in
-      // a register and written as one unaligned dword (+ one byte): bytes
-      // past the header are overwritten by the literals / offset after it
-      const int rem = (L - 15) & 255;
-      const int le = L >= 15 ? (rem == 255 ? 2 : 1) : 0;
+      const int tm = M == 0 ? 0 : (M >= 19 ? 15 : mx);                // LZ4.c:542
+      // token, u16 size, literal-extension bytes (LZ4.c:367-386) as one
+      // unaligned dword + a zero 5th byte: bytes past the header are this
+      // sequence's literals / offset, written after it
       const uint32_t ext = rem == 255 ? 255u : (uint32_t)rem;         // [255, 0] or [rem]
-      const uint64_t hdrw = (uint64_t)((tl << 4) | tm) | ((uint64_t)(SZ & 0xFFFF) << 8) |
-                            ((uint64_t)ext << 24);                    // 5th byte: 0
-      *reinterpret_cast<u32u *>(S.buf + o) = (uint32_t)hdrw;
-      if (le == 2) S.buf[o + 4] = 0;
+      const uint32_t SZ = (ws >> 16) & 0xFFFFu;
+      *reinterpret_cast<u32u *>(S.buf + o) = (uint32_t)((tl << 4) | tm) | (SZ << 8) | (ext << 24);
+      S.buf[o + 4] = 0;
       o += 3 + le;
       // literals (LZ4.c:388): the lane copies its own run, 16 bytes per
       // step, the last piece exact (8/4/2/1) so no lane writes past its run;
@@ -581,10 +568,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
         if (m & 1) *d = (uint8_t)lo;
       }
       o += L;
-      // offset (LZ4.c:390) and match extension (LZ4.c:393-411)
-      const bool mext = M >= 4 && ((M - 4) & 255) >= 15;
+      // offset (LZ4.c:390) and match extension (LZ4.c:393-411); without one
+      // the byte goes to the lane's dword of the idle candidate list
       *reinterpret_cast<u16u *>(S.buf + o) = (uint16_t)D;
-      if (mext) S.buf[o + 2] = (uint8_t)(((M - 4) & 255) - 15);
+      *(mextW ? S.buf + o + 2 : reinterpret_cast<uint8_t *>(&S.cand[lane])) = (uint8_t)(mx - 15);
     }
     ocar += (int)(tot & 0xFFFFu);
     szsum += (int)(tot >> 16);
