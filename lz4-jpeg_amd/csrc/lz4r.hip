@@ -105,8 +105,13 @@ constexpr int kCand = 128;               // candidate list (drained when a pass 
 
 static_assert(kInOff % 16 == 0 && kTileIn % 4 == 0, "4/8/16-B staging");
 
-constexpr int kSlot = kBlkOutMax;         // scratch bytes per block slot (16-B multiple)
-static_assert(kSlot % 16 == 0 && kBlkOutMax / 16 <= 64, "aligned slots, one store round");
+#ifndef LZ4R_SLOT
+#define LZ4R_SLOT 560
+#endif
+// scratch bytes per block slot (640-B line-aligned slots measured the same)
+constexpr int kSlot = LZ4R_SLOT;
+static_assert(kSlot % 16 == 0 && kSlot >= kBlkOutMax && kBlkOutMax / 16 <= 64,
+              "aligned slots, one store round");
 
 struct TileLds {
   alignas(16) uint8_t buf[kRegion];
@@ -858,7 +863,7 @@ void free_scratch(lz4r_ctx *c) {
   (void)hipFree(c->tsz);
   (void)hipFree(c->gsum);
   (void)hipFree(c->part);
-  if (c->slots) (void)hipFree(c->slots - 16);
+  if (c->slots) (void)hipFree(c->slots);
   c->bsizes = nullptr;
   c->slots = nullptr;
   c->tsz = nullptr;
@@ -873,12 +878,12 @@ int ensure_scratch(lz4r_ctx *c, size_t nb) {
   const size_t cap = nb + nb / 8 + 1024;
   const size_t parts = (cap + kPart - 1) / kPart;
   const size_t groups = (cap + kGT - 1) / kGT;
-  uint8_t *slots = nullptr;      // 16-B pad in front: gather reads slot - 16
-  if (hipMalloc(&slots, cap * (size_t)kSlot + 32) != hipSuccess) {
+  uint8_t *slots = nullptr;      // hipMalloc: 256-B aligned, so every slot is line-aligned
+  if (hipMalloc(&slots, cap * (size_t)kSlot) != hipSuccess) {
     free_scratch(c);
     return LZ4R_ERR_NOMEM;
   }
-  c->slots = slots + 16;
+  c->slots = slots;
   if (hipMalloc(&c->bsizes, cap * sizeof(uint16_t)) != hipSuccess ||
       hipMalloc(&c->tsz, cap * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&c->gsum, groups * sizeof(uint32_t)) != hipSuccess ||
