@@ -8,11 +8,11 @@
 // Blocks are independent; the compressor is one compute kernel plus a cheap
 // placement pass:
 //
-// lz4_tiles: workgroup = one wave = one tile of kTB consecutive blocks
-// (default 1: 5.1 KB of LDS, <= 64 VGPRs -> 8 waves per SIMD; occupancy is
-// what this issue/latency-bound kernel lives on).  Per tile:
-//   stage    tile bytes -> LDS (widest aligned loads: the only read of the input).
-//   per block, position-parallel (lane owns p = 64r + lane, r < 5):
+// lz4_tiles: workgroup = one wave = one 300-B block (5.1 KB of LDS, <= 64
+// VGPRs -> 8 waves per SIMD; occupancy is what this issue-bound kernel lives
+// on).  Per block:
+//   stage    the block's 75 dwords -> LDS (the only read of the input).
+//   position-parallel, blocked (lane l owns p = 5 l .. 5 l + 4):
 //     index  per-bucket chains of the 4-gram starts by a 9-bit hash: p swaps
 //            itself into its bucket's u16 head (ds_mskor_rtn_b32 on a dword of
 //            two heads) and keeps the old head as its link;
@@ -29,24 +29,25 @@
 //              best(p) = lexmax over q <= p of (q + local_len(q), q - local_j(q))
 //            i.e. the longest match ends furthest right and, among equals,
 //            has the largest distance (= smallest source, LZ4.c:307).  One
-//            wave max-scan (DPP) over the positions gives best() for all p.
-//            M = len & 0xFF (the uint8_t return, LZ4.c:317).
-//     parse  nm(x) = first matchable position >= x (ballot masks);
-//            succ(c) = nm(c + M(c)); the greedy parse (LZ4.c:516-583) is the
-//            walk c0 = nm(0), c_{k+1} = succ(c_k), one LDS read per sequence.
-//     emit   sequence k on lane k: sizes, wave scan for offsets, token /
-//            size / literal-extension / offset bytes (write_sequence,
-//            LZ4.c:365-413) and its literal run (16-B unaligned LDS copies),
-//            into the block's LDS output area.
-//     store  the block's bytes -> its 16-B aligned scratch slot (one round of
+//            wave max-scan gives best() for all p.  M = len & 0xFF (the
+//            uint8_t return, LZ4.c:317).
+//     parse  nm(x) = first matchable position >= x; succ(c) = nm(c + M(c));
+//            the greedy parse (LZ4.c:516-583) is the walk c0 = nm(0),
+//            c_{k+1} = succ(c_k), three sequences per LDS round trip through
+//            the jump table succ | succ^2 | succ^3.
+//   emit     sequence k on lane k: one packed wave scan of the bytes written
+//            and the size fields, token / size / literal-extension / offset
+//            bytes (write_sequence, LZ4.c:365-413) and its literal run (16-B
+//            unaligned LDS copies), into the block's LDS output area.
+//   store    the block's bytes -> its 16-B aligned scratch slot (one round of
 //            16-B stores), its size -> usz (u32, for the scan) and bsizes (u16).
 // lz4_scan_reduce / lz4_scan_partials: exclusive scan of the block sizes.
 // lz4_gather: 32 blocks per workgroup: slots -> LDS image of the output
 // range (unaligned LDS stores) -> aligned 16-B global stores.
 // No workgroup ever waits on another (a fused decoupled look-back ran the
-// waves in lock-step at the pace of the slowest tile of each round).
-// HBM traffic per input byte: 1 B read + ~1.03 B written by lz4_tiles, and
-// ~1.03 B read + ~1.03 B written by lz4_gather (+6 B/block of block sizes).
+// waves in lock-step at the pace of the slowest block of each round).
+// HBM traffic per input byte: 1 B read + ~1.1 B written by lz4_tiles, and
+// ~1.1 B read + ~1.03 B written by lz4_gather (+6 B/block of block sizes).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -59,36 +60,19 @@
 
 // LZ4R_VARIANT (timing ablations only, never shipped): 1 = no match search,
 // 2 = no index/match phase, 3 = index only (no candidates), 4 = candidates
-// without the lcp verification, 6 = input from a 150 KB hot set, 10 = no
-// literal scatter, 11 = no sequence emission and no literal scatter (isolates the
-// HBM fetch: 7.27 vs 7.00 ms on 1 GiB -- the fetch is hidden by occupancy)
+// without the lcp verification, 11 = no sequence emission.
 #ifndef LZ4R_VARIANT
 #define LZ4R_VARIANT 0
 #endif
 
-#ifdef LZ4R_PROF
-__device__ unsigned long long g_prof[16];
-__device__ __forceinline__ uint64_t prof_now() {
-  uint64_t t;
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
-  return t;
-}
-#define PROF_T(i) do { const uint64_t _t = prof_now(); prof[i] += _t - prof_last; prof_last = _t; } while (0)
-#else
-#define PROF_T(i) do { } while (0)
-#endif
 
 namespace {
 
 constexpr int kBlk = LZ4R_BLOCK;          // 300
-#ifndef LZ4R_TB
-#define LZ4R_TB 1
-#endif
-constexpr int kTB = LZ4R_TB;              // blocks per tile
 #ifndef LZ4R_WPE
 #define LZ4R_WPE
 #endif
-constexpr int kTileIn = kTB * kBlk;       // staged input bytes per tile
+constexpr int kTileIn = kBlk;             // staged input bytes (one block)
 constexpr int kBlkOutMax = 560;           // >= 548: worst-case bytes of one block, 16-B multiple
 // LDS byte region: the block being encoded writes its bytes at buf[0 ..
 // kBlkOutMax); the tile's input sits at kInOff + 300k; then an over-read pad.
@@ -103,7 +87,7 @@ constexpr int kArr = kBlk + 4;
 constexpr int kQ = kBlk;                 // walker ring (<= one live walker per entry)
 constexpr int kCand = 128;               // candidate list (drained when a pass could fill it)
 
-static_assert(kInOff % 16 == 0 && kTileIn % 4 == 0, "4/8/16-B staging");
+static_assert(kInOff % 16 == 0 && kBlk == 75 * 4, "dword staging: 75 dwords");
 
 #ifndef LZ4R_SLOT
 #define LZ4R_SLOT 560
@@ -242,11 +226,9 @@ __device__ __forceinline__ void wave_sync() {
 
 // Encode block `k` of the tile (n bytes at S.buf[kInOff + 300k]) into
 // S.buf[obase ...]; returns the bytes written.
-__device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
-                                            uint64_t *prof, uint64_t &prof_last) {
-  (void)prof; (void)prof_last;
+__device__ __forceinline__ int encode_block(TileLds &S, int n) {
   const int lane = threadIdx.x;
-  const int base = kInOff + k * kBlk;
+  constexpr int base = kInOff;
   constexpr int obase = 0;
 
   // ---- index: per-bucket chains of the 4-gram starts -----------------------
@@ -324,7 +306,6 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
   }
   wave_sync();
 
-  PROF_T(0);
   // ---- candidates: walk the chains ------------------------------------------
   // A pair (j < p) of one bucket is a candidate when the tags agree and the
   // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]).  Candidates go to
@@ -383,9 +364,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     }
     if (ncand) drain();
   }
-  PROF_T(1);
   wave_sync();
-  PROF_T(2);
   // ---- best(p) = prefix lexmax of (end, dist) -------------------------------
   // blocked: a running max over the lane's five positions, one wave scan of
   // the lane totals, the exclusive prefix folded back in
@@ -460,7 +439,6 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
   }
   wave_sync();
 
-  PROF_T(3);
   // ---- greedy parse = walk over match starts (LZ4.c:516-583) ---------------
   // The walk is the serial part of the block: from c0 = nm(0), each step
   // reads the jump-table word of the last recorded start (three more starts)
@@ -507,7 +485,6 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
   int e = 0;                             // end of the last match
   if (Sv) e = last + (int)(__builtin_amdgcn_readfirstlane(S.rec[last]) & 255u);
   wave_sync();
-  PROF_T(4);
   // ---- sequences: lane kk = sequence kk ------------------------------------
   const int nseq = Sv + (e < n ? 1 : 0);
   int ocar = 3;                      // block header: u8 nseq, u16 size
@@ -588,91 +565,47 @@ __device__ __forceinline__ int encode_block(TileLds &S, int k, int n,
     S.buf[obase + 2] = (uint8_t)((bsz >> 8) & 255);
   }
   wave_sync();
-  PROF_T(5);
   return ocar;
 }
 
 __global__ __launch_bounds__(64) LZ4R_WPE void lz4_tiles(
-    const uint8_t *__restrict__ in, size_t n_total, size_t nb_total, size_t t_first,
-    size_t ntiles, uint8_t *__restrict__ slots, uint32_t *__restrict__ usz,
-    uint16_t *__restrict__ bsizes) {
+    const uint8_t *__restrict__ in, uint32_t nb, uint32_t per, uint32_t last_n,
+    uint8_t *__restrict__ slots, uint32_t *__restrict__ usz, uint16_t *__restrict__ bsizes) {
   __shared__ TileLds S;
   const int lane = threadIdx.x;
-  uint64_t prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#ifdef LZ4R_PROF
-  uint64_t prof_last = prof_now();
-#else
-  uint64_t prof_last = 0;
-#endif
-
   // XCD-aware order: workgroups w and w + 8 share an XCD (observed round-robin
   // dealing), so XCD w % 8 takes the contiguous slice [(w % 8) per, ...) of
   // the blocks and a 128-B line shared by two neighbouring blocks is fetched
   // into one L2, not two (a speed matter only: any mapping is correct).
-  const size_t per = (ntiles - t_first + 7) / 8;
-#ifndef LZ4R_XCD
-#define LZ4R_XCD 1
-#endif
-  const size_t t_mine = LZ4R_XCD ? t_first + (blockIdx.x & 7) * per + (blockIdx.x >> 3)
-                                 : t_first + blockIdx.x;
-  for (size_t t = t_mine; t < ntiles; t = ntiles) {   // one tile per workgroup
-    const size_t b0 = t * kTB;
-    const int nbt = (int)min((size_t)kTB, nb_total - b0);
-    const size_t byte0 = b0 * kBlk;
-    const int len = (int)min((size_t)kTileIn, n_total - byte0);
-    // variant 6: every tile reads one of the first 64 tiles (input hot in L2)
-    const uint8_t *src = in + (LZ4R_VARIANT == 6 && byte0 + 64 * (size_t)kTileIn < n_total
-                                   ? (t % 64) * (size_t)kTileIn : byte0);
+  const uint32_t t = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  if (t >= nb) return;
+  const int n = t == nb - 1 ? (int)last_n : kBlk;
+  const uint8_t *src = in + (size_t)t * kBlk;
 
-    // ---- stage the tile (16-B loads) ---------------------------------------
-    {
-      uint8_t *dst = S.buf + kInOff;
-      int done = 0;
-      if (((uintptr_t)src & 15) == 0) {
-        const int nvec = len >> 4;
-        for (int i = lane; i < nvec; i += 64)
-          reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
-        done = nvec * 16;
-      } else if (((uintptr_t)src & 7) == 0) {   // 2-block tiles start 8-B aligned
-        const int nvec = len >> 3;
-        for (int i = lane; i < nvec; i += 64)
-          reinterpret_cast<uint2 *>(dst)[i] = reinterpret_cast<const uint2 *>(src)[i];
-        done = nvec * 8;
-      } else if (((uintptr_t)src & 3) == 0) {   // 1-block tiles start 4-B aligned
-        const int nvec = len >> 2;
-        for (int i = lane; i < nvec; i += 64)
-          reinterpret_cast<uint32_t *>(dst)[i] = reinterpret_cast<const uint32_t *>(src)[i];
-        done = nvec * 4;
-      }
-      for (int i = done + lane; i < len; i += 64) dst[i] = src[i];
-      if (lane < 16) dst[len + lane] = 0;
+  // ---- stage the block: 75 dwords, both loads in flight; 16-B zero pad ------
+  {
+    uint32_t *dst = reinterpret_cast<uint32_t *>(S.buf + kInOff);
+    if (n == kBlk && ((uintptr_t)in & 3) == 0) {
+      const uint32_t *q = reinterpret_cast<const uint32_t *>(src);
+      const uint32_t v0 = q[lane];
+      const uint32_t v1 = lane < 11 ? q[64 + lane] : 0u;
+      dst[lane] = v0;
+      if (lane < 15) dst[64 + lane] = v1;
+    } else {
+      for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
+      if (lane < 16) S.buf[kInOff + n + lane] = 0;
     }
-    wave_sync();
-
-    // ---- encode the tile's blocks; each leaves for its slot at once ---------
-    for (int k = 0; k < nbt; ++k) {
-      const size_t gb = b0 + k;
-      const int n = (gb == nb_total - 1) ? (int)(n_total - gb * kBlk) : kBlk;
-      PROF_T(7);
-      const int W = encode_block(S, k, n, prof, prof_last);
-      PROF_T(8);
-      // the block's bytes -> its 16-B aligned slot (<= 35 chunks: one round);
-      // the next block overwrites buf[0 ..) only after these LDS reads (in order)
-      uint4 *dst = reinterpret_cast<uint4 *>(slots + gb * (size_t)kSlot);
-      if (lane < ((W + 15) >> 4)) dst[lane] = reinterpret_cast<const uint4 *>(S.buf)[lane];
-      if (lane == 0) {
-        usz[gb] = (uint32_t)W;
-        bsizes[gb] = (uint16_t)W;
-      }
-      PROF_T(9);
-    }
-    wave_sync();                                // LDS reused by the next tile
-    PROF_T(9);
   }
-#ifdef LZ4R_PROF
-  if (lane == 0)
-    for (int i = 0; i < 10; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof[i]);
-#endif
+  wave_sync();
+
+  const int W = encode_block(S, n);
+  // the block's bytes -> its 16-B aligned slot (<= 35 chunks: one round)
+  uint4 *dst = reinterpret_cast<uint4 *>(slots + (size_t)t * kSlot);
+  if (lane < ((W + 15) >> 4)) dst[lane] = reinterpret_cast<const uint4 *>(S.buf)[lane];
+  if (lane == 0) {
+    usz[t] = (uint32_t)W;
+    bsizes[t] = (uint16_t)W;
+  }
 }
 
 // ---- placement: exclusive scan of tile sizes, then gather -----------------
@@ -904,7 +837,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   int rc = ensure_scratch(c, nb);
   if (rc != LZ4R_OK) return rc;
   if (nb > 0xffffffffULL || n > (1ull << 37)) return LZ4R_ERR_ARG;
-  static_assert(kTB == 1 && kPart % kGT == 0, "tiles are blocks; partials hold whole groups");
+  static_assert(kPart % kGT == 0, "partials hold whole groups");
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool timed = c->timing;
   c->timed_call = timed;
@@ -913,9 +846,10 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   // per-tile cost (a static grid-stride split leaves a tail; measured slower
   // also with the next block prefetched into registers)
   static const unsigned extra_lds = getenv("LZ4R_EXTRA_LDS") ? (unsigned)atoi(getenv("LZ4R_EXTRA_LDS")) : 0u;
-  hipLaunchKernelGGL(lz4_tiles, dim3((unsigned)(8 * ((nb + 7) / 8))), dim3(64), extra_lds, s,
-                     static_cast<const uint8_t *>(d_in), n, nb, (size_t)0, nb, c->slots, c->tsz,
-                     c->bsizes);
+  const uint32_t per = (uint32_t)((nb + 7) / 8);       // blocks per XCD slice
+  hipLaunchKernelGGL(lz4_tiles, dim3(8 * per), dim3(64), extra_lds, s,
+                     static_cast<const uint8_t *>(d_in), (uint32_t)nb, per,
+                     (uint32_t)(n - (nb - 1) * kBlk), c->slots, c->tsz, c->bsizes);
   if (timed) (void)hipEventRecord(c->ev_b, s);
   const size_t nparts = (nb + kPart - 1) / kPart;
   hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)nparts), dim3(256), 0, s, c->tsz, nb,
@@ -938,11 +872,6 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
 
 extern "C" {
 
-#ifdef LZ4R_PROF
-int lz4r_debug_prof(unsigned long long *out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 int lz4r_ctx_create(lz4r_ctx **out) {
   if (!out) return LZ4R_ERR_ARG;
