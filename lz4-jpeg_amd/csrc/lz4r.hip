@@ -295,14 +295,22 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
     }
   }
   wave_sync();                       // the heads are dead: the queue overlays them
-  int qwr = 0;                           // walkers queued (S.q[0 .. qwr))
+  // queue the walkers lane-major: one wave scan of the per-lane counts
+  int qwr;                               // walkers queued (S.q[0 .. qwr))
+  {
+    int cnt = 0;
 #pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const bool walk = item[r] != 0u;     // p != link, so a walker's item is never 0
-    const uint64_t wm = ballot(walk);
-    // branch-free: lanes without a walker write their own dword of the idle cand list
-    *(walk ? &S.q[qwr + rank_below(wm)] : &S.cand[lane]) = item[r];
-    qwr += __popcll(wm);
+    for (int r = 0; r < 5; ++r) cnt += item[r] != 0u;   // p != link: a walker's item is never 0
+    const uint32_t inc = wave_incl_add((uint32_t)cnt);
+    qwr = (int)__builtin_amdgcn_readlane((int)inc, 63);
+    int at = (int)inc - cnt;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const bool walk = item[r] != 0u;
+      // branch-free: lanes without a walker write their own dword of the idle cand list
+      *(walk ? &S.q[at] : &S.cand[lane]) = item[r];
+      at += walk;
+    }
   }
   wave_sync();
 
@@ -372,7 +380,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     const int p = p0 + r;
-    const uint32_t rv = p < n ? S.rec[p] : 0u;
+    const uint32_t rv = S.rec[min(p, kArr - 1)];        // 0 at and past n (zeroed above)
     const int bl = (int)(rv >> 9), bj = 511 - (int)(rv & 511u);
     v[r] = bl >= 4 ? (((uint32_t)(p + bl) << 9) | (uint32_t)(p - bj)) : 0u;
     if (r) v[r] = max(v[r], v[r - 1]);
