@@ -464,47 +464,45 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
     ++it;
     c = (int)(t >> 18);
   }
-  // sequence list: S.seq[0] = c0, S.seq[1 + 3 i + f] = field f of word i
-  if (lane == 0) S.seq[0] = (uint32_t)F0;
-  int Sv = F0 < n ? 1 : 0, last = F0;    // starts recorded; the last one
-  if (it <= 64) {
-    if (lane < it) {
-      S.seq[1 + 3 * lane] = seqv & 511u;
-      S.seq[2 + 3 * lane] = (seqv >> 9) & 511u;
-      S.seq[3 + 3 * lane] = seqv >> 18;
-    }
-    if (it) {                            // only the last word can hold n's
-      const uint32_t tl = __builtin_amdgcn_readlane(seqv, it - 1);
-      const int a = (int)(tl & 511u), b = (int)((tl >> 9) & 511u), d = (int)(tl >> 18);
-      const int cprev = it >= 2 ? (int)(__builtin_amdgcn_readlane(seqv, it - 2) >> 18) : F0;
-      Sv += 3 * (it - 1) + (a < n) + (b < n) + (d < n);
-      last = d < n ? d : b < n ? b : a < n ? a : cprev;
-    }
-  } else {                               // rare (truncated matches): walk again into the LDS
+  // Sequence k's match start: k = 0 -> c0, k = 1 + 3 i + f -> field f of word
+  // i (lane i of seqv), n past the last match.  Past 64 words (> 193
+  // sequences, only with truncated matches) the walk is redone into S.seq.
+  const bool slow = it > 64;
+  int Sv_slow = 0;
+  if (slow) {
+    if (lane == 0) S.seq[0] = (uint32_t)F0;
+    Sv_slow = 1;
     for (c = F0; c < n;) {
       const uint32_t t = __builtin_amdgcn_readfirstlane(S.jt[c]);
       const int a = (int)(t & 511u), b = (int)((t >> 9) & 511u), d = (int)(t >> 18);
-      if (lane >= 1 && lane <= 3) S.seq[Sv + lane - 1] = lane == 1 ? a : lane == 2 ? b : d;
-      Sv += (a < n) + (b < n) + (d < n);
-      last = d < n ? d : b < n ? b : a < n ? a : last;
+      if (lane >= 1 && lane <= 3) S.seq[Sv_slow + lane - 1] = lane == 1 ? a : lane == 2 ? b : d;
+      Sv_slow += (a < n) + (b < n) + (d < n);
       c = d;
     }
+    wave_sync();
   }
-  int e = 0;                             // end of the last match
-  if (Sv) e = last + (int)(__builtin_amdgcn_readfirstlane(S.rec[last]) & 255u);
-  wave_sync();
   // ---- sequences: lane kk = sequence kk ------------------------------------
-  const int nseq = Sv + (e < n ? 1 : 0);
+  // A round is 64 consecutive sequences; the match sequences are a prefix
+  // (cpos < n), followed by the literal-only tail when the last match ends
+  // before n (LZ4.c:585-612).  Rounds go on while a round is all matches.
+  int nseq = 0;
   int ocar = 3;                      // block header: u8 nseq, u16 size
   int szsum = 0;
   int end_prev = 0;                  // end of the previous round's last match
-  for (int s0 = 0; s0 < nseq && LZ4R_VARIANT != 11; s0 += 64) {
+  for (int s0 = 0; LZ4R_VARIANT != 11; s0 += 64) {
     const int kk = s0 + lane;
-    const bool act = kk < nseq;
-    const bool ism = kk < Sv;                                      // ends with a match
-    // branch-free reads: entries past Sv are garbage, clamped and discarded
-    const uint32_t cq = min(S.seq[min(kk, kArr - 1)], (uint32_t)(kArr - 1));
-    const uint32_t rv = S.rec[cq];
+    uint32_t cq;
+    if (!slow) {
+      const int km = kk - 1, i = (km * 21846) >> 16, f = km - 3 * i;   // km / 3 (km < 32768)
+      const uint32_t w = (uint32_t)__shfl((int)seqv, i & 63, 64);
+      cq = kk == 0 ? (uint32_t)F0 : (i < it ? (w >> (9 * f)) & 511u : (uint32_t)n);
+    } else {
+      cq = kk < Sv_slow ? S.seq[kk] : (uint32_t)n;
+    }
+    const bool ism = (int)cq < n;                                  // ends with a match
+    const uint64_t mm = ballot(ism);
+    const int nm_r = __popcll(mm);                                 // a prefix of the round
+    const uint32_t rv = S.rec[min(cq, (uint32_t)(kArr - 1))];
     const int cpos = ism ? (int)cq : n;
     const int M = ism ? (int)(rv & 255u) : 0;
     const int D = ism ? (int)((rv >> 8) & 511u) : 0;             // the tail writes offset 0
@@ -513,6 +511,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
     const int pend = lane == 0 ? end_prev : (int)upv;             // literal run start
     end_prev = (int)lane63((uint32_t)end);
     const int L = cpos - pend;
+    const bool act = ism || (lane == nm_r && pend < n);            // the tail: literals left
     // bytes written (LZ4.c:365-413) and the size field (LZ4.c:546-575), which
     // differ for M = 1..3: the field counts a match-extension byte that
     // write_sequence never writes
@@ -565,6 +564,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
     }
     ocar += (int)(tot & 0xFFFFu);
     szsum += (int)(tot >> 16);
+    nseq += (int)__popcll(ballot(act));
+    if (nm_r < 64) break;
   }
   if (lane == 0) {                                                     // LZ4.c:417-419
     const int bsz = szsum + 3;
