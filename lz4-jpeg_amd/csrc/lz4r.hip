@@ -318,7 +318,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
   // A pair (j < p) of one bucket is a candidate when the tags agree and the
   // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]).  Candidates go to
   // a list in S.cand, drained by a balanced lcp pass with LDS atomicMax into
-  // S.rec (len << 9 | 511 - j: the longest, ties to the smallest j).
+  // S.rec ((p + len) << 9 | (p - j): the longest, ties to the smallest j).
   if (search && LZ4R_VARIANT != 3) {
     constexpr int kTrash = kCand - 1;
     int ncand = 0;
@@ -328,7 +328,9 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
         const uint32_t pr = S.cand[i];
         const int p = (int)(pr & 0xFFFFu), j = (int)(pr >> 16);
         const int l = lcp(S.buf, base + j, base + p, n - p);
-        if (l >= 4) atomicMax(&S.rec[p], ((uint32_t)l << 9) | (uint32_t)(511 - j));
+        // (end, dist) as the best scan wants it: for one p the larger end is
+        // the longer match and the larger dist the smaller source
+        if (l >= 4) atomicMax(&S.rec[p], ((uint32_t)(p + l) << 9) | (uint32_t)(p - j));
       }
       wave_sync();
     };
@@ -379,10 +381,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
   uint32_t v[5];
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
-    const int p = p0 + r;
-    const uint32_t rv = S.rec[min(p, kArr - 1)];        // 0 at and past n (zeroed above)
-    const int bl = (int)(rv >> 9), bj = 511 - (int)(rv & 511u);
-    v[r] = bl >= 4 ? (((uint32_t)(p + bl) << 9) | (uint32_t)(p - bj)) : 0u;
+    // local(p) as end << 9 | dist; 0 without a candidate and at and past n
+    v[r] = S.rec[min(p0 + r, kArr - 1)];
     if (r) v[r] = max(v[r], v[r - 1]);
   }
   {
