@@ -157,8 +157,12 @@ __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
     const uint64_t x1 = *reinterpret_cast<const u64u *>(d + a + l + 8) ^
                         *reinterpret_cast<const u64u *>(d + b + l + 8);
     diff = (x0 | x1) != 0;
-    const int at = x0 ? (__builtin_ctzll(x0) >> 3) : 8 + (__builtin_ctzll(x1 | (1ull << 63)) >> 3);
-    l += diff ? at : 16;
+    // first differing byte, branch-free (a select, not an exec-masked if/else)
+    const uint32_t a0 = (uint32_t)__builtin_ctzll(x0 | (1ull << 63)) >> 3;
+    const uint32_t a1 = 8u + ((uint32_t)__builtin_ctzll(x1 | (1ull << 63)) >> 3);
+    const uint32_t m0 = 0u - (uint32_t)(x0 != 0);
+    const uint32_t at = (a0 & m0) | (a1 & ~m0);
+    l += diff ? (int)at : 16;
   } while (!diff && l < limit);
   return l < limit ? l : limit;
 }
