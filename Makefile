@@ -22,7 +22,7 @@ OBJS    := $(B)/lz4r.o $(B)/lz4r_gpudec.o $(B)/jpegr.o $(B)/jpegr_blocks.o $(B)/
            $(B)/synth.o \
            $(B)/lz4r_decode.o $(B)/compat.o
 
-all: lib bin oracle
+all: lib bin oracle tools
 
 lib: $(LIB)
 
@@ -57,8 +57,15 @@ $(BIN)/%.exe: $(BIN)/%
 oracle:
 	$(MAKE) -C oracle
 
+# issue-rate micro-benchmark for the instruction-issue roof (tools/issue.sh)
+tools: tools/variants/valu_rate
+
+tools/variants/valu_rate: tools/valu_rate.hip
+	@mkdir -p tools/variants
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -o $@ $<
+
 clean:
 	rm -rf $(B) $(BIN) $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib bin oracle clean
+.PHONY: all lib bin oracle tools clean

@@ -31,6 +31,39 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # (tools/traffic.sh -> tools/traffic_summary.py, gfx950 FETCH correction applied)
 TRAFFIC_JSON = os.path.join(REPO, "profiles", "r01_traffic.json")
+# per-launch instruction counts of lz4_tiles + measured SIMD issue rates
+# (tools/issue.sh -> tools/issue_summary.py)
+ISSUE_JSON = os.path.join(REPO, "profiles", "r01_issue.json")
+
+
+def issue_roof(bytes_now, launch_ms):
+    """The compressor's binding roof: wave-instruction issue.  Counts per
+    launch from PMC (scaled to this input), rates from the micro-benchmark."""
+    try:
+        d = json.load(open(ISSUE_JSON))
+        pl, rates = d["lz4"]["per_launch"], d["issue_rates_winstr_per_s"]
+        scale = bytes_now / d["lz4"]["bytes_per_launch"]
+        valu = pl["SQ_INSTS_VALU"] * scale
+        salu = pl["SQ_INSTS_SALU"] * scale
+        peak_mix = rates["4 valu + 4 salu"]
+        peak_valu = rates["v_add/xor/and/or"]
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
+    sec = launch_ms / 1e3
+    return {
+        "bound": "issue (VALU + SALU wave-instructions)", "unit": "Gwinstr/s",
+        "achieved": round((valu + salu) / sec / 1e9, 1), "peak": round(peak_mix / 1e9, 1),
+        "frac": round((valu + salu) / sec / peak_mix, 4),
+        "valu_frac": round(valu / sec / peak_valu, 4),
+        "per_block": {"valu": round(pl["SQ_INSTS_VALU"] / pl["SQ_WAVES"], 1),
+                      "salu": round(pl["SQ_INSTS_SALU"] / pl["SQ_WAVES"], 1),
+                      "lds": round(pl["SQ_INSTS_LDS"] / pl["SQ_WAVES"], 1),
+                      "branch": round(pl["SQ_INSTS_BRANCH"] / pl["SQ_WAVES"], 1)},
+        "note": "achieved = PMC SQ_INSTS_VALU + SQ_INSTS_SALU per launch (profiles/r01_issue.json, "
+                "scaled to this input) / lz4_tiles time; peak = the chip's measured rate for an "
+                "interleaved 4 VALU + 4 SALU stream at 8 waves per SIMD (tools/valu_rate.hip); "
+                "valu_frac = VALU alone against the measured v_add rate",
+    }
 
 
 def measured_traffic(kind, bytes_now, bytes_profiled):
@@ -189,6 +222,7 @@ def main():
         "achieved": round(n / (avg_match_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
         "unit": "GB/s", "frac": round(n / (avg_match_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
         "traffic": measured_traffic("lz4", n, 1 << 30),
+        "binding_roof": issue_roof(n, avg_match_ms),
         "algorithmic_bytes_per_launch": n,
         "avg_launch_ms": round(avg_match_ms, 4),
         "whole_call_ms": round(avg_call_ms, 4),
