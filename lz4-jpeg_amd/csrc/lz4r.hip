@@ -9,8 +9,8 @@
 // placement pass:
 //
 // lz4_tiles: workgroup = one wave = one 300-B block (5.1 KB of LDS, <= 64
-// VGPRs -> 8 waves per SIMD; occupancy is what this issue-bound kernel lives
-// on).  Per block:
+// VGPRs -> 8 waves per SIMD; occupancy is what this LDS- and issue-bound
+// kernel lives on).  Per block:
 //   stage    the block's 75 dwords -> LDS (the only read of the input).
 //   position-parallel, blocked (lane l owns p = 5 l .. 5 l + 4):
 //     index  per-bucket chains of the 4-gram starts by a 9-bit hash: p swaps
@@ -18,8 +18,8 @@
 //            two heads) and keeps the old head as its link;
 //            entry = link | preceding byte << 9 | tag << 17.
 //     local  every unordered pair of a bucket is met once, by the later-
-//            inserted entry walking its chain; walkers that go on are
-//            re-queued, so every pass is balanced over the lanes.  A pair
+//            inserted entry walking its chain; a lane keeps its walker until
+//            the chain ends and then takes the next queued one.  A pair
 //            (j < p) is a candidate when the tags agree and it is
 //            LEFT-MAXIMAL (j == 0 or blk[j-1] != blk[p-1]); a balanced lcp
 //            pass takes the longest candidate per p, ties to the smallest j
@@ -37,13 +37,15 @@
 //            the jump table succ | succ^2 | succ^3.
 //   emit     sequence k on lane k: one packed wave scan of the bytes written
 //            and the size fields, token / size / literal-extension / offset
-//            bytes (write_sequence, LZ4.c:365-413) and its literal run (16-B
-//            unaligned LDS copies), into the block's LDS output area.
+//            bytes (write_sequence, LZ4.c:365-413); the literal runs
+//            flattened over the lanes as aligned 8-byte words.  Every byte
+//            lands in the zeroed LDS output area by an aligned ds_or: a
+//            misaligned LDS access is replayed at ~1-2 cycles per lane.
 //   store    the block's bytes -> its 16-B aligned scratch slot (one round of
 //            16-B stores), its size -> usz (u32, for the scan) and bsizes (u16).
 // lz4_scan_reduce / lz4_scan_partials: exclusive scan of the block sizes.
-// lz4_gather: 32 blocks per workgroup: slots -> LDS image of the output
-// range (unaligned LDS stores) -> aligned 16-B global stores.
+// lz4_gather: 32 blocks per workgroup: slots -> zeroed LDS image of the
+// output range (aligned ds_or of shifted chunks) -> aligned 16-B global stores.
 // No workgroup ever waits on another (a fused decoupled look-back ran the
 // waves in lock-step at the pace of the slowest block of each round).
 // HBM traffic per input byte: 1 B read + ~1.1 B written by lz4_tiles, and
@@ -106,7 +108,7 @@ struct TileLds {
   };
   union {
     uint32_t ent[kArr];   // per position: link | preceding byte << 9 | tag << 17
-    uint16_t nm[kArr];    // then: first matchable position >= x
+    uint32_t nm[kArr];    // then: first matchable position >= x (dwords: no sub-dword LDS access)
     uint32_t jt[kArr];    // then: succ, succ^2, succ^3 of a match start (9 bits each)
   };
   uint32_t rec[kArr];     // local(p) accumulator; then M | dist<<8 | succ<<17
@@ -141,13 +143,14 @@ __device__ __forceinline__ void mskor_rtn5(uint32_t (&old)[5], const uint32_t (&
 }
 
 typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned LDS access (the LDS
-typedef uint32_t u32u __attribute__((aligned(1)));   // runs in unaligned mode)
-typedef uint16_t u16u __attribute__((aligned(1)));
+                                                     // runs in unaligned mode; replayed)
 
 // Longest common prefix of the byte runs at a and b (a < b), capped at
 // `limit` = n - b: the canonical clamp (a match never crosses the block end).
-// 8-byte words as unaligned ds_read_b64 (the LDS runs in unaligned mode);
-// reads past the region land in its pad (>= 16 B past any block end).
+// 8-byte words as unaligned ds_read_b64 (the LDS runs in unaligned mode;
+// an aligned-read + funnel-shift variant cut the LDS replays but cost more
+// VALU than it saved); reads past the region land in its pad (>= 16 B past
+// any block end).
 __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
   int l = 0;
   bool diff;
@@ -165,6 +168,14 @@ __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
     l += diff ? (int)at : 16;
   } while (!diff && l < limit);
   return l < limit ? l : limit;
+}
+
+// OR the (<= 4) bytes of v into the zeroed byte area at offset x: two
+// aligned dwords (ds_or_b32), never a misaligned access
+__device__ __forceinline__ void or_bytes(uint32_t *buf32, int x, uint32_t v) {
+  const uint64_t w = (uint64_t)v << (8 * (x & 3));
+  atomicOr(&buf32[x >> 2], (uint32_t)w);
+  atomicOr(&buf32[(x >> 2) + 1], (uint32_t)(w >> 32));
 }
 
 // DPP helpers (gfx9 row_shr / row_bcast; identity 0 for lanes without a source)
@@ -338,39 +349,33 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
       }
       wave_sync();
     };
-    // ring of walkers: a pass reads up to 64, then queues those that go on
-    // (at most one walker per entry is ever live: <= kQ)
-    int qrd = 0, live = qwr;
-    qwr = qwr == kQ ? 0 : qwr;
-    while (live > 0) {
-      const int m = live < 64 ? live : 64;
-      const bool act = lane < m;
-      int qi = qrd + lane;
-      qi -= qi >= kQ ? kQ : 0;
-      const uint32_t it = act ? S.q[qi] : 0u;
-      const int a = (int)(it & 0xFFFFu), b = (int)(it >> 16);   // a walks, b < ... in chain
+    // Persistent walkers: a lane keeps its walker (a walks, b = the next chain
+    // entry) in registers until the chain ends, and an idle lane takes the
+    // next queued walker.  The queue is read once, front to back: no ring,
+    // no re-queue stores.
+    int qrd = 0;
+    int a = 0, b = 0;
+    bool valid = false;
+    for (;;) {
+      const uint64_t em = ballot(!valid);
+      const int idx = qrd + rank_below(em);
+      const bool need = !valid && idx < qwr;
+      const uint32_t it = S.q[min(idx, kQ - 1)];
+      a = need ? (int)(it & 0xFFFFu) : a;
+      b = need ? (int)(it >> 16) : b;
+      valid = valid || need;
+      if (ballot(valid) == 0) break;       // no walker left and the queue is empty
+      qrd += __popcll(em);
       const uint32_t me = S.ent[a], o = S.ent[b];
       const uint32_t x = me ^ o;
       const int p = max(a, b), j = min(a, b);
-      const bool cand = act && (x >> 17) == 0 && (j == 0 || (x & (255u << 9)) != 0);
+      const bool cand = valid && (x >> 17) == 0 && (j == 0 || (x & (255u << 9)) != 0);
       const uint64_t cm = ballot(cand);
-      const int sl = cand ? ncand + rank_below(cm) : kTrash;
-      S.cand[sl] = (uint32_t)p | ((uint32_t)j << 16);
+      const int sl = cand ? ncand + rank_below(cm) : kTrash;   // one shared trash slot:
+      S.cand[sl] = (uint32_t)p | ((uint32_t)j << 16);           // same-address stores cost nothing
       ncand += __popcll(cm);
-      const uint32_t nx = o & 511u;
-      const bool go = act && nx != 511u;
-      const uint64_t gm = ballot(go);
-      if (go) {
-        int wi = qwr + rank_below(gm);
-        wi -= wi >= kQ ? kQ : 0;
-        S.q[wi] = (uint32_t)a | (nx << 16);
-      }
-      const int ng = __popcll(gm);
-      qrd += m;
-      qrd -= qrd >= kQ ? kQ : 0;
-      qwr += ng;
-      qwr -= qwr >= kQ ? kQ : 0;
-      live += ng - m;
+      b = (int)(o & 511u);                 // 511: the chain ended (ent[511] still lies
+      valid = valid && b != 511;           // inside TileLds; an idle lane's loads are unused)
       if (ncand > kTrash - 64) {
         drain();
         ncand = 0;
@@ -418,7 +423,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
     for (int r = 4; r >= 0; --r) f[r] = (mrec[r] & 255u) ? p0 + r : f[r + 1];
 #pragma unroll
     for (int r = 0; r < 5; ++r)
-      S.nm[min(p0 + r, kArr - 1)] = (uint16_t)f[r];   // past n: unused
+      S.nm[min(p0 + r, kArr - 1)] = f[r];   // past n: unused
   }
   wave_sync();
   // succ(p) = nm(p + M(p)) for the match starts; succ(n) = n.  Then the
@@ -489,6 +494,9 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
   // A round is 64 consecutive sequences; the match sequences are a prefix
   // (cpos < n), followed by the literal-only tail when the last match ends
   // before n (LZ4.c:585-612).  Rounds go on while a round is all matches.
+  if (lane < kBlkOutMax / 16)          // the output area starts zeroed: bytes land by ds_or
+    reinterpret_cast<uint4 *>(S.buf)[lane] = make_uint4(0, 0, 0, 0);
+  wave_sync();
   int nseq = 0;
   int ocar = 3;                      // block header: u8 nseq, u16 size
   int szsum = 0;
@@ -529,42 +537,57 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
     const uint32_t inc = wave_incl_add(ws);
     const uint32_t tot = lane63(inc);
     const int excl = (int)((inc - ws) & 0xFFFFu);
+    // Every LDS access of the emission is naturally aligned (a misaligned
+    // ds_read/ds_write is replayed by the LDS at ~1-2 cycles per lane): the
+    // output area is zeroed and every byte lands by an aligned ds_or.
+    const int o = obase + ocar + excl;
+    const int ol = o + 3 + le;                                         // first literal byte
+    uint32_t *const out32 = reinterpret_cast<uint32_t *>(S.buf);
     if (act) {
-      int o = obase + ocar + excl;
       const int tl = L >= 15 ? 15 : L;                                // LZ4.c:540
       const int tm = M == 0 ? 0 : (M >= 19 ? 15 : mx);                // LZ4.c:542
-      // token, u16 size, literal-extension bytes (LZ4.c:367-386) as one
-      // unaligned dword + a zero 5th byte: bytes past the header are this
-      // sequence's literals / offset, written after it
-      const uint32_t ext = rem == 255 ? 255u : (uint32_t)rem;         // [255, 0] or [rem]
+      // token, u16 size, literal-extension bytes (LZ4.c:367-386): [rem] or [255, 0]
+      const uint32_t ext = le == 0 ? 0u : (rem == 255 ? 255u : (uint32_t)rem);
       const uint32_t SZ = (ws >> 16) & 0xFFFFu;
-      *reinterpret_cast<u32u *>(S.buf + o) = (uint32_t)((tl << 4) | tm) | (SZ << 8) | (ext << 24);
-      S.buf[o + 4] = 0;
-      o += 3 + le;
-      // literals (LZ4.c:388): the lane copies its own run, 16 bytes per
-      // step, the last piece exact (8/4/2/1) so no lane writes past its run;
-      // the block's input is never overlaid while its output is written
-      const uint8_t *ls = S.buf + base + pend;
-      for (int i = 0; i < L; i += 16) {
-        uint64_t lo = *reinterpret_cast<const u64u *>(ls + i);
-        const uint64_t hi = *reinterpret_cast<const u64u *>(ls + i + 8);
-        uint8_t *d = S.buf + o + i;
-        const int m = L - i;
-        if (m >= 16) {
-          *reinterpret_cast<u64u *>(d) = lo;
-          *reinterpret_cast<u64u *>(d + 8) = hi;
-          continue;
+      or_bytes(out32, o, (uint32_t)((tl << 4) | tm) | (SZ << 8) | (ext << 24));
+      // offset (LZ4.c:390) and match extension (LZ4.c:393-411)
+      or_bytes(out32, ol + L, (uint32_t)D | (mextW ? ((uint32_t)(mx - 15) & 255u) << 16 : 0u));
+    }
+    // literals (LZ4.c:388), flattened over the lanes: one aligned 8-byte
+    // output word per lane and round, its bytes funnel-shifted out of two
+    // aligned input words and masked to the run
+    {
+      const int cw = act && L > 0 ? ((ol + L - 1) >> 3) - (ol >> 3) + 1 : 0;   // words of the run
+      const uint32_t cinc = wave_incl_add((uint32_t)cw);
+      const int C = (int)lane63(cinc), st = (int)cinc - cw;
+      const uint32_t prm = (uint32_t)ol | ((uint32_t)L << 10) | ((uint32_t)pend << 19);
+      uint32_t carry = 0;                        // 1 + the last run owning a word so far
+      for (int g0 = 0; g0 < C; g0 += 64) {
+        wave_sync();
+        S.cand[lane] = 0u;                       // run-start marks of this round
+        if (cw > 0 && st >= g0 && st < g0 + 64) S.cand[st - g0] = (uint32_t)lane + 1u;
+        wave_sync();                             // marks of other lanes: no forwarding
+        const uint32_t k1 = max(wave_incl_max(S.cand[lane]), carry);
+        carry = lane63(k1);
+        const int g = g0 + lane;
+        const int k = (int)k1 - 1;               // the run owning word g
+        const uint32_t pk = (uint32_t)__shfl((int)prm, k & 63, 64);
+        const int sk = __shfl(st, k & 63, 64);
+        if (g < C) {
+          const int kol = (int)(pk & 1023u), kL = (int)((pk >> 10) & 511u);
+          const int kpend = (int)(pk >> 19);
+          const int w = (kol >> 3) + (g - sk);                         // output word
+          const int xs = 8 * w + base + kpend - kol;                   // its input bytes
+          const uint64_t *iw = reinterpret_cast<const uint64_t *>(S.buf + (xs & ~7));
+          const uint64_t lo = iw[0], hi = iw[1];
+          const uint32_t sh = 8u * (uint32_t)(xs & 7);
+          const uint64_t v = (lo >> sh) | ((hi << 1) << (63u - sh));
+          const int lb = max(kol - 8 * w, 0), hb = min(kol + kL - 8 * w, 8);
+          const uint64_t mask = (~0ull << (8 * lb)) & (~0ull >> (64 - 8 * hb));
+          atomicOr(reinterpret_cast<unsigned long long *>(S.buf + 8 * w),
+                   (unsigned long long)(v & mask));
         }
-        if (m & 8) { *reinterpret_cast<u64u *>(d) = lo; d += 8; lo = hi; }
-        if (m & 4) { *reinterpret_cast<u32u *>(d) = (uint32_t)lo; d += 4; lo >>= 32; }
-        if (m & 2) { *reinterpret_cast<u16u *>(d) = (uint16_t)lo; d += 2; lo >>= 16; }
-        if (m & 1) *d = (uint8_t)lo;
       }
-      o += L;
-      // offset (LZ4.c:390) and match extension (LZ4.c:393-411); without one
-      // the byte goes to the lane's dword of the idle candidate list
-      *reinterpret_cast<u16u *>(S.buf + o) = (uint16_t)D;
-      *(mextW ? S.buf + o + 2 : reinterpret_cast<uint8_t *>(&S.cand[lane])) = (uint8_t)(mx - 15);
     }
     ocar += (int)(tot & 0xFFFFu);
     szsum += (int)(tot >> 16);
@@ -733,6 +756,14 @@ __global__ __launch_bounds__(256) void lz4_gather(
   const uint64_t G0 = toff[h0];
   const uintptr_t abs0 = (uintptr_t)(out + G0);
   const int lead = (int)(abs0 & 15);               // img[lead] = stream byte G0
+  // zero the image: every byte then lands by an aligned ds_or (a misaligned
+  // LDS store is replayed at ~2 cycles per lane)
+  {
+    const int span = lead + (int)(toff[h1] - G0);
+    for (int i = tid; i < (span + 15) >> 4; i += 256)
+      reinterpret_cast<uint4 *>(img)[i] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
   // ---- slots -> LDS image -----------------------------------------------------
   {
     constexpr int kPer = kGH / 4;                  // slots per wave
@@ -744,19 +775,18 @@ __global__ __launch_bounds__(256) void lz4_gather(
         while (t + 1 < s1 && (int)cex[t + 1] <= c) ++t;
         const int j = c - (int)cex[t];
         const uint4 v = reinterpret_cast<const uint4 *>(slots + (g0 + t) * (size_t)kSlot)[j];
-        uint8_t *d = img + lead + (int)(toff[t] - G0) + 16 * j;
+        const int x = lead + (int)(toff[t] - G0) + 16 * j;      // image byte of the chunk
         const int m = (int)(toff[t + 1] - toff[t]) - 16 * j;   // bytes of this slot left
         uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
-        const uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
-        if (m >= 16) {
-          *reinterpret_cast<u64u *>(d) = lo;
-          *reinterpret_cast<u64u *>(d + 8) = hi;
-        } else {
-          if (m & 8) { *reinterpret_cast<u64u *>(d) = lo; d += 8; lo = hi; }
-          if (m & 4) { *reinterpret_cast<u32u *>(d) = (uint32_t)lo; d += 4; lo >>= 32; }
-          if (m & 2) { *reinterpret_cast<u16u *>(d) = (uint16_t)lo; d += 2; lo >>= 16; }
-          if (m & 1) *d = (uint8_t)lo;
-        }
+        uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+        lo &= m >= 8 ? ~0ull : (1ull << (8 * m)) - 1ull;          // m >= 1
+        hi &= m >= 16 ? ~0ull : (m <= 8 ? 0ull : (1ull << (8 * (m - 8))) - 1ull);
+        // the 16 bytes shifted by x & 7 over three aligned 8-byte words
+        const uint32_t sh = 8u * (uint32_t)(x & 7);
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(img + (x & ~7));
+        atomicOr(&w[0], (unsigned long long)(lo << sh));
+        atomicOr(&w[1], (unsigned long long)((hi << sh) | ((lo >> 1) >> (63u - sh))));
+        atomicOr(&w[2], (unsigned long long)((hi >> 1) >> (63u - sh)));
       }
     }
   }
