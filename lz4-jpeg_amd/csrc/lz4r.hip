@@ -149,8 +149,8 @@ typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned LDS access (th
 // `limit` = n - b: the canonical clamp (a match never crosses the block end).
 // 8-byte words as unaligned ds_read_b64 (the LDS runs in unaligned mode;
 // an aligned-read + funnel-shift variant cut the LDS replays but cost more
-// VALU than it saved); reads past the region land in its pad (>= 16 B past
-// any block end).
+// VALU than it saved, and 8 bytes per step measured the same); reads past
+// the region land in its pad (>= 16 B past any block end).
 __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
   int l = 0;
   bool diff;
@@ -559,7 +559,9 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
     {
       const int cw = act && L > 0 ? ((ol + L - 1) >> 3) - (ol >> 3) + 1 : 0;   // words of the run
       const uint32_t cinc = wave_incl_add((uint32_t)cw);
-      const int C = (int)lane63(cinc), st = (int)cinc - cw;
+      // exclusive prefix by a lane shift (cinc - cw made the compiler keep
+      // every partial of the scan to re-add them)
+      const int C = (int)lane63(cinc), st = (int)dpp<0x138, 0xf, 0xf>(cinc);
       const uint32_t prm = (uint32_t)ol | ((uint32_t)L << 10) | ((uint32_t)pend << 19);
       uint32_t carry = 0;                        // 1 + the last run owning a word so far
       for (int g0 = 0; g0 < C; g0 += 64) {
