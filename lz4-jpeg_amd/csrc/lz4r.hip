@@ -229,6 +229,14 @@ __device__ __forceinline__ int rank_below(uint64_t m) {
 
 
 
+// per lane: t where the lane's bit of m is set, else f (v_cndmask with the
+// mask straight from an SGPR pair)
+__device__ __forceinline__ uint32_t sel_mask(uint64_t m, uint32_t t, uint32_t f) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  return r;
+}
+
 // The compressor's workgroup is one wave.  A wave's LDS operations are
 // served in order, so its phase boundaries need neither s_barrier nor the
 // s_waitcnt vmcnt(0) lgkmcnt(0) that __syncthreads() implies: a compiler
@@ -353,29 +361,34 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
     // entry) in registers until the chain ends, and an idle lane takes the
     // next queued walker.  The queue is read once, front to back: no ring,
     // no re-queue stores.
+    // The walkers' liveness is kept as a scalar lane mask: a ballot of a
+    // loop-carried bool costs two VALU (v_cndmask + v_cmp) per use, and the
+    // selects take the mask straight from SGPRs (every mask here is last
+    // written by a SALU op: no VALU-SGPR hazard)
     int qrd = 0;
     int a = 0, b = 0;
-    bool valid = false;
+    uint64_t vm = 0;                       // lanes holding a walker
     for (;;) {
-      const uint64_t em = ballot(!valid);
+      const uint64_t em = ~vm;
       const int idx = qrd + rank_below(em);
-      const bool need = !valid && idx < qwr;
+      const uint64_t nm_ = em & ballot(idx < qwr);
       const uint32_t it = S.q[min(idx, kQ - 1)];
-      a = need ? (int)(it & 0xFFFFu) : a;
-      b = need ? (int)(it >> 16) : b;
-      valid = valid || need;
-      if (ballot(valid) == 0) break;       // no walker left and the queue is empty
+      a = (int)sel_mask(nm_, it & 0xFFFFu, (uint32_t)a);
+      b = (int)sel_mask(nm_, it >> 16, (uint32_t)b);
+      vm |= nm_;
+      if (vm == 0) break;                  // no walker left and the queue is empty
       qrd += __popcll(em);
       const uint32_t me = S.ent[a], o = S.ent[b];
       const uint32_t x = me ^ o;
       const int p = max(a, b), j = min(a, b);
-      const bool cand = valid && (x >> 17) == 0 && (j == 0 || (x & (255u << 9)) != 0);
-      const uint64_t cm = ballot(cand);
-      const int sl = cand ? ncand + rank_below(cm) : kTrash;   // one shared trash slot:
-      S.cand[sl] = (uint32_t)p | ((uint32_t)j << 16);           // same-address stores cost nothing
+      // a ballot of each compare (a ballot of a combined bool costs two VALU)
+      const uint64_t cm =
+          vm & ballot((x >> 17) == 0) & (ballot(j == 0) | ballot((x & (255u << 9)) != 0));
+      const int sl = (int)sel_mask(cm, (uint32_t)(ncand + rank_below(cm)), (uint32_t)kTrash);
+      S.cand[sl] = (uint32_t)p | ((uint32_t)j << 16);
       ncand += __popcll(cm);
-      b = (int)(o & 511u);                 // 511: the chain ended (ent[511] still lies
-      valid = valid && b != 511;           // inside TileLds; an idle lane's loads are unused)
+      b = (int)(o & 511u);
+      vm &= ballot(b != 511);
       if (ncand > kTrash - 64) {
         drain();
         ncand = 0;
