@@ -15,7 +15,9 @@
 // occupancy (19.5 KB of LDS per wave: the 64 output slots; 8 waves/CU) and
 // keeps instruction counts low:
 //   - the lane reads its encoded bytes with single unaligned 8/16-byte
-//     global loads (L1/L2 absorb the re-reads of the wave's ~20 KB range);
+//     global loads (L1/L2 absorb the re-reads of the wave's ~20 KB range),
+//     after touching the block's next four 128-B lines up front so that the
+//     serial walk does not wait on HBM once per line;
 //   - a sequence header is decoded branch-free for the plain reading; the
 //     rare truncated readings (below) take a separate path;
 //   - literals move in 16-byte chunks; a match of distance D is copied in
@@ -55,6 +57,8 @@ constexpr int kInMax = LZ4R_BLOCK_BOUND;   // bytes of one encoded block (bound)
 constexpr int kLanes = 64;                 // blocks per workgroup (one wave)
 constexpr int kDepth = 10;                 // choice points per lane (<= 9 needed)
 constexpr int kMaxSteps = 1 << 16;         // header budget: a hostile stream cannot spin a lane
+constexpr int kPfN = 4;                    // L2 lines touched ahead of the walk
+constexpr int kPfS = 128;                  // (2 / 4 / 8 lines, 64 or 128 B apart: same time)
 
 typedef uint64_t u64u __attribute__((aligned(1)));
 typedef uint32_t u32u __attribute__((aligned(1)));
@@ -330,12 +334,25 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
   const size_t b = b0 + lane;
 
   int q = 0;                                         // decoded bytes (0 = failed / absent)
+  uint32_t pfv[kPfN] = {};
   if (lane < nl) {
     const bool last = b == nb - 1;
     const size_t beg = 1 + boff[b];
     const size_t end = last ? in_len : 1 + boff[b + 1];
     if (end >= beg + 3 && end <= in_len && end - beg <= (size_t)kInMax) {
       const Slot o{S.out + lane * kBlk};
+      // touch the block's next four 128-B lines now: the walk's header loads
+      // then hit L2 instead of waiting on HBM one line at a time (the values
+      // are folded into pfx after the walk; 1.82 -> 1.66 ms per GiB)
+      {
+        const uint8_t *q0 = in + ((beg + kPfS) & ~(size_t)(kPfS - 1));
+        const uint8_t *qe = in + end;
+#pragma unroll
+        for (int t = 0; t < kPfN; ++t) {
+          const uint8_t *q = q0 + kPfS * t;
+          pfv[t] = *(q < qe ? q : q0 - kPfS);          // one byte: never past the stream
+        }
+      }
       // a read reaches at most kInMax + 32 bytes past the wave's first block
       if (1 + boff[b0] + (size_t)(kLanes + 1) * kInMax + 64 <= in_len)
         q = decode_block(Bytes<false>{in + beg, in_len - beg}, (int)(end - beg), last, o);
@@ -345,6 +362,11 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
     if (q == 0) atomicMin(&result[1], (unsigned long long)b + 1);
     else if (last) result[0] = (unsigned long long)(b * kBlk + q);
   }
+  // keeps the prefetch loads alive; never true for a decoded block (q <= 300)
+  uint32_t pfx = 0;
+#pragma unroll
+  for (int t = 0; t < kPfN; ++t) pfx ^= pfv[t];
+  if (pfx == 0x5A5A5A5Au && q == 1000) q = 0;
   S.qlen[lane] = (uint32_t)q;
   __syncthreads();
 
