@@ -57,12 +57,16 @@ $(BIN)/%.exe: $(BIN)/%
 oracle:
 	$(MAKE) -C oracle
 
-# issue-rate micro-benchmark for the instruction-issue roof (tools/issue.sh)
-tools: tools/variants/valu_rate
+# micro-benchmarks: SIMD issue rates (tools/issue.sh) and LDS access costs
+tools: tools/variants/valu_rate tools/variants/lds_rate
 
 tools/variants/valu_rate: tools/valu_rate.hip
 	@mkdir -p tools/variants
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -o $@ $<
+
+tools/variants/lds_rate: tools/lds_rate.hip
+	@mkdir -p tools/variants
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -Wno-unused-result -o $@ $<
 
 clean:
 	rm -rf $(B) $(BIN) $(LIB)
