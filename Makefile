@@ -17,9 +17,10 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -ffp-contract=off -fPIC -std=c++17 -Wall 
             -Wno-unused-result
 CFLAGS_HOST := -O2 -fPIC -Wall -std=gnu11 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
 LIB     := $(PKG)/lz4jpeg/liblz4jpeg.so
-HDRS    := include/lz4r.h include/jpegr.h include/lz4jpeg_compat.h $(CSRC)/jpeg_tables.h
+HDRS    := include/lz4r.h include/jpegr.h include/lz4jpeg_compat.h include/lz4jpeg_synth.h \
+           $(CSRC)/jpeg_tables.h
 OBJS    := $(B)/lz4r.o $(B)/lz4r_gpudec.o $(B)/jpegr.o $(B)/jpegr_blocks.o $(B)/jpegr_entropy.o \
-           $(B)/synth.o \
+           $(B)/synth.o $(B)/synth_dev.o \
            $(B)/lz4r_decode.o $(B)/compat.o
 
 all: lib bin oracle tools

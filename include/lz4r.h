@@ -49,6 +49,10 @@ extern "C" {
 #define LZ4R_ERR_NOMEM (-5)       /* device allocation failed */
 #define LZ4R_ERR_CORRUPT (-6)     /* decoder: malformed stream */
 
+/* Inputs up to 2^40 bytes per call; the kernels run in chunks of 2^24 blocks
+ * (5.03 GB), so device scratch is ~9.4 GB of block slots at most plus
+ * 16 B per block of the whole input. */
+
 typedef struct lz4r_ctx lz4r_ctx;
 
 /* Create a context bound to the current HIP device. */
@@ -74,14 +78,17 @@ int lz4r_compress_async(lz4r_ctx *ctx, const void *d_in, size_t n,
                         void *d_out, size_t cap, void *d_out_len,
                         void *stream);
 
-/* A run of whole 300-byte blocks (n need not be a multiple of 300 only for
- * the globally last shard) without the frame header byte, for shards of a
- * multi-GPU job; asynchronous, length at d_out_len like lz4r_compress_async.
+/* A run of whole 300-byte blocks without the frame header byte, for shards
+ * of a multi-GPU job; asynchronous, length at d_out_len like
+ * lz4r_compress_async.  Only the globally last shard (final_shard != 0) may
+ * end in a short block: a non-final shard whose n is not a multiple of 300
+ * is rejected with LZ4R_ERR_ARG (its stream would differ from the single-GPU
+ * one).  n == 0 (more ranks than blocks) enqueues a zero length.
  * Concatenating the segments of consecutive shards after one header byte
  * (u8 total_blocks & 0xFF) yields the single-GPU stream. */
 int lz4r_compress_segment_async(lz4r_ctx *ctx, const void *d_in, size_t n,
                                 void *d_out, size_t cap, void *d_out_len,
-                                void *stream);
+                                int final_shard, void *stream);
 
 /* After a compress call: copy the encoded byte count (uint16) of each of the
  * first `count` blocks of the last call to `dst` (host or device memory),
@@ -93,10 +100,17 @@ int lz4r_copy_block_sizes(const lz4r_ctx *ctx, void *dst, size_t count,
 /* After a compress call: copy the first `count` per-block output offsets
  * (uint64, exclusive scan, relative to the first block byte -- add 1 for a
  * framed stream) of the last call to `dst` (host or device memory), then
- * synchronise `stream`.  Used for sampled per-block parity checks at full
- * size. */
+ * synchronise `stream`.  The placement kernel writes them on the device as
+ * it computes them (8 B/block); no host prefix sum. */
 int lz4r_copy_block_offsets(const lz4r_ctx *ctx, void *dst, size_t count,
                             void *stream);
+
+/* The same offsets in place: *d_offsets = the context's device array of the
+ * last call's *count block offsets (valid until the next call on ctx; ready
+ * when the call's stream reaches its end).  This is what the block-parallel
+ * decoder takes, without a host round trip. */
+int lz4r_block_offsets_device(const lz4r_ctx *ctx, const void **d_offsets,
+                              size_t *count);
 
 /* Decode a framed stream (bytes as lz4r_compress writes them) back to the
  * input.  Host C; replaces LZ4_decode / interpret_frame (LZ4.c:937-1121),
@@ -127,9 +141,10 @@ int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
                   size_t *out_len);
 
 /* Measurement: when enabled, every compress call records HIP events on its
- * own launch stream around the whole call and around the compressor kernel
- * (lz4_tiles, the only kernel of the call).  lz4r_last_timing waits for the
- * last call's end event and returns both durations in milliseconds. */
+ * own launch stream around the whole call and around each launch of the
+ * compressor kernel lz4_tiles (one per 2^24-block chunk of the input).
+ * lz4r_last_timing waits for the last call's end event and returns the
+ * call's duration and the summed lz4_tiles durations in milliseconds. */
 int lz4r_set_timing(lz4r_ctx *ctx, int enable);
 int lz4r_last_timing(lz4r_ctx *ctx, float *ms_call, float *ms_match);
 

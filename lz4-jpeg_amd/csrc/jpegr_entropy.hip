@@ -480,10 +480,15 @@ __global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
   // (2-byte stores to 64 scattered streams wrote ~6x the bytes)
   int16_t *o = S.out[lane];
   const int n = stream_len(c);
-  const bool ok = U <= kDecCap
-                      ? decode_stream(b, m, t, Col<uint32_t>{&S.lc[0][lane], kLanes},
-                                      Col<uint32_t>{&S.vl[0][lane], kLanes}, o, n)
-                      : decode_stream_slow(b, m, t, o, n);
+  // a foreign or corrupted meta word must not index past the stream's slot:
+  // its bits (bits_cap bits) and its table (2 n entries: RLE of n ints)
+  const bool sane = (int)(m & 0xFFFF) <= bits_cap(c) && U <= 2 * n;
+  const bool ok = sane && (U <= kDecCap
+                               ? decode_stream(b, m, t, Col<uint32_t>{&S.lc[0][lane], kLanes},
+                                               Col<uint32_t>{&S.vl[0][lane], kLanes}, o, n)
+                               : decode_stream_slow(b, m, t, o, n));
+  if (!sane)
+    for (int j = 0; j < n; ++j) o[j] = 0;
   if (!ok) atomicAdd(&status[1], 1u);
   uint4 *dst = reinterpret_cast<uint4 *>(coef + tile * 128 + coef_off(c));
   const uint4 *src = reinterpret_cast<const uint4 *>(o);

@@ -60,7 +60,9 @@
 
 #include "../../include/lz4r.h"
 
-// LZ4R_VARIANT (timing ablations only, never shipped): 1 = no match search,
+// LZ4R_VARIANT: per-phase timing ablations for the instruction budget in
+// DESIGN.md, compiled only by tools/build_variants.sh into tools/variants/
+// (the Makefile's product build never defines it): 1 = no match search,
 // 2 = no index/match phase, 3 = index only (no candidates), 4 = candidates
 // without the lcp verification, 11 = no sequence emission.
 #ifndef LZ4R_VARIANT
@@ -71,19 +73,13 @@
 namespace {
 
 constexpr int kBlk = LZ4R_BLOCK;          // 300
-#ifndef LZ4R_WPE
-#define LZ4R_WPE
-#endif
 constexpr int kTileIn = kBlk;             // staged input bytes (one block)
 constexpr int kBlkOutMax = 560;           // >= 548: worst-case bytes of one block, 16-B multiple
 // LDS byte region: the block being encoded writes its bytes at buf[0 ..
 // kBlkOutMax); the tile's input sits at kInOff + 300k; then an over-read pad.
 constexpr int kInOff = kBlkOutMax;
 constexpr int kRegion = kInOff + kTileIn + 48;  // + over-read pad (lcp, 32-B copy reads)
-#ifndef LZ4R_HB
-#define LZ4R_HB 9
-#endif
-constexpr int kHB = LZ4R_HB;              // hash bits: 512 buckets
+constexpr int kHB = 9;                    // hash bits: 512 buckets
 constexpr int kH = 1 << kHB;
 constexpr int kArr = kBlk + 4;
 constexpr int kQ = kBlk;                 // walker ring (<= one live walker per entry)
@@ -91,11 +87,8 @@ constexpr int kCand = 128;               // candidate list (drained when a pass 
 
 static_assert(kInOff % 16 == 0 && kBlk == 75 * 4, "dword staging: 75 dwords");
 
-#ifndef LZ4R_SLOT
-#define LZ4R_SLOT 560
-#endif
 // scratch bytes per block slot (640-B line-aligned slots measured the same)
-constexpr int kSlot = LZ4R_SLOT;
+constexpr int kSlot = 560;
 static_assert(kSlot % 16 == 0 && kSlot >= kBlkOutMax && kBlkOutMax / 16 <= 64,
               "aligned slots, one store round");
 
@@ -619,7 +612,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
   return ocar;
 }
 
-__global__ __launch_bounds__(64) LZ4R_WPE void lz4_tiles(
+__global__ __launch_bounds__(64) void lz4_tiles(
     const uint8_t *__restrict__ in, uint32_t nb, uint32_t per, uint32_t last_n,
     uint8_t *__restrict__ slots, uint32_t *__restrict__ usz, uint16_t *__restrict__ bsizes) {
   __shared__ TileLds S;
@@ -731,16 +724,14 @@ __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__
 // writes its W % 16 bytes exactly, so slots never overwrite each other).
 // Then the range leaves as aligned 16-B stores; only the group's two edge
 // chunks are written bytewise.  Also writes the frame byte (LZ4.c:429).
-#ifndef LZ4R_GH
-#define LZ4R_GH 32
-#endif
-constexpr int kGH = LZ4R_GH;                         // blocks per gather workgroup
+constexpr int kGH = 32;                              // blocks per gather workgroup
 constexpr int kGSplit = kGT / kGH;                   // workgroups per group
 constexpr int kGatherLds = kGH * kBlkOutMax + 32;    // worst case: every block 548 B
 __global__ __launch_bounds__(256) void lz4_gather(
-    const uint8_t *__restrict__ slots, const uint32_t *__restrict__ tsz, size_t ntiles,
-    size_t g_first, const uint32_t *__restrict__ gsum, const uint64_t *__restrict__ part,
-    uint8_t *__restrict__ out, uint64_t cap, int hdr, uint64_t nb_total) {
+    const uint8_t *__restrict__ slots, size_t slot_base, const uint32_t *__restrict__ tsz,
+    size_t ntiles, size_t g_first, const uint32_t *__restrict__ gsum,
+    const uint64_t *__restrict__ part, uint8_t *__restrict__ out, uint64_t cap, int hdr,
+    uint64_t nb_total, uint64_t *__restrict__ boff) {
   __shared__ uint64_t toff[kGT + 1];
   __shared__ uint32_t cex[kGT + 1];                  // exclusive chunk counts
   __shared__ alignas(16) uint8_t img[kGatherLds];
@@ -761,6 +752,9 @@ __global__ __launch_bounds__(256) void lz4_gather(
     const uint32_t inc = wave_incl_add(v);
     toff[tid] = base + inc - v;
     if (tid == 63) toff[kGT] = base + inc;
+    // device-resident block offsets (relative to the first block byte) for
+    // the block-parallel decoder: no host prefix sum, no host round trip
+    if (h0 == 0 && tid < nt) boff[g0 + tid] = base + inc - v - (uint64_t)hdr;
     const uint32_t ck = (tid >= h0 && tid < h1) ? (v + 15u) >> 4 : 0u;
     const uint32_t cinc = wave_incl_add(ck);
     cex[tid] = cinc - ck;
@@ -789,7 +783,8 @@ __global__ __launch_bounds__(256) void lz4_gather(
       for (int c = c0 + lane; c < c1; c += 64) {
         while (t + 1 < s1 && (int)cex[t + 1] <= c) ++t;
         const int j = c - (int)cex[t];
-        const uint4 v = reinterpret_cast<const uint4 *>(slots + (g0 + t) * (size_t)kSlot)[j];
+        const uint4 v =
+            reinterpret_cast<const uint4 *>(slots + (g0 + t - slot_base) * (size_t)kSlot)[j];
         const int x = lead + (int)(toff[t] - G0) + 16 * j;      // image byte of the chunk
         const int m = (int)(toff[t + 1] - toff[t]) - 16 * j;   // bytes of this slot left
         uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
@@ -831,18 +826,37 @@ __global__ __launch_bounds__(256) void lz4_gather(
 
 }  // namespace
 
+// Launch chunking: lz4_tiles is a 64-lane workgroup per block, and a HIP
+// grid may not exceed 2^32 work-items, so a call is cut into chunks of at
+// most kChunk blocks (5.03 GB of input; a multiple of the scan partial, so
+// every chunk starts on a gather group and a partial).  The block slots are
+// sized for one chunk (9.4 GB at most) and reused; the per-block arrays and
+// the scan state span the whole call.  Each chunk is a full compress ->
+// scan -> gather pass that continues the stream offset the previous chunk
+// left in *d_len; the per-chunk launch cost (four launches) is noise against
+// the ~19 ms of encoder work in a full chunk.
+constexpr size_t kChunk = size_t(1) << 24;
+static_assert(kChunk % kPart == 0, "chunks start on a scan partial");
+static_assert((kChunk / 8) * 8 * 64 < (size_t(1) << 32), "chunk grid fits HIP's limit");
+// largest input one call accepts (block indices are u32 in the per-call arrays)
+constexpr size_t kMaxInput = size_t(1) << 40;
+
 struct lz4r_ctx {
   int device = 0;
-  size_t cap_blocks = 0;       // capacity of the per-block arrays
+  size_t cap_blocks = 0;       // capacity of the per-call per-block arrays
+  size_t cap_slots = 0;        // capacity of the slot scratch, in blocks (<= kChunk)
   uint16_t *bsizes = nullptr;  // encoded bytes of every block of the last call
-  uint8_t *slots = nullptr;    // per-block output slots (kSlot bytes each)
+  uint64_t *boff = nullptr;    // every block's offset from the first block byte
+  uint8_t *slots = nullptr;    // per-block output slots (kSlot bytes each), one chunk
   uint32_t *tsz = nullptr;     // encoded bytes per block (u32, for the scan)
-  uint32_t *gsum = nullptr;    // encoded bytes per group of kGT tiles
-  uint64_t *part = nullptr;    // scan partials, one per kPart tiles
-  unsigned max_grid = 0;       // resident workgroups of lz4_tiles on this device
+  uint32_t *gsum = nullptr;    // encoded bytes per group of kGT blocks
+  uint64_t *part = nullptr;    // scan partials, one per kPart blocks
   uint64_t *len = nullptr;     // default device length slot
   size_t last_nb = 0;
-  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr;
+  // timing: the call's start/end, and lz4_tiles' start/end in every chunk
+  hipEvent_t ev_a = nullptr, ev_c = nullptr;
+  std::vector<hipEvent_t> ev_tiles;   // 2 per chunk
+  size_t timed_chunks = 0;
   bool timing = false;
   bool timed_call = false;     // the last call recorded the events
 };
@@ -851,73 +865,96 @@ namespace {
 
 void free_scratch(lz4r_ctx *c) {
   (void)hipFree(c->bsizes);
+  (void)hipFree(c->boff);
   (void)hipFree(c->tsz);
   (void)hipFree(c->gsum);
   (void)hipFree(c->part);
-  if (c->slots) (void)hipFree(c->slots);
+  (void)hipFree(c->slots);
   c->bsizes = nullptr;
+  c->boff = nullptr;
   c->slots = nullptr;
   c->tsz = nullptr;
   c->gsum = nullptr;
   c->part = nullptr;
   c->cap_blocks = 0;
+  c->cap_slots = 0;
 }
 
 int ensure_scratch(lz4r_ctx *c, size_t nb) {
-  if (nb <= c->cap_blocks) return LZ4R_OK;
+  const size_t need_slots = std::min(nb, kChunk);
+  if (nb <= c->cap_blocks && need_slots <= c->cap_slots) return LZ4R_OK;
   free_scratch(c);
   const size_t cap = nb + nb / 8 + 1024;
+  const size_t cap_slots = std::min(cap, kChunk);
   const size_t parts = (cap + kPart - 1) / kPart;
   const size_t groups = (cap + kGT - 1) / kGT;
-  uint8_t *slots = nullptr;      // hipMalloc: 256-B aligned, so every slot is line-aligned
-  if (hipMalloc(&slots, cap * (size_t)kSlot) != hipSuccess) {
-    free_scratch(c);
-    return LZ4R_ERR_NOMEM;
-  }
-  c->slots = slots;
-  if (hipMalloc(&c->bsizes, cap * sizeof(uint16_t)) != hipSuccess ||
+  // hipMalloc: 256-B aligned, so every slot is line-aligned
+  if (hipMalloc(&c->slots, cap_slots * (size_t)kSlot) != hipSuccess ||
+      hipMalloc(&c->bsizes, cap * sizeof(uint16_t)) != hipSuccess ||
+      hipMalloc(&c->boff, cap * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&c->tsz, cap * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&c->gsum, groups * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&c->part, parts * sizeof(uint64_t)) != hipSuccess) {
+    (void)hipGetLastError();
     free_scratch(c);
     return LZ4R_ERR_NOMEM;
   }
   c->cap_blocks = cap;
+  c->cap_slots = cap_slots;
   return LZ4R_OK;
 }
 
+int ensure_events(lz4r_ctx *c, size_t nchunks) {
+  while (c->ev_tiles.size() < 2 * nchunks) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return LZ4R_ERR_HIP;
+    c->ev_tiles.push_back(e);
+  }
+  return LZ4R_OK;
+}
+
+// hdr = 1: a framed stream (frame byte first).  hdr = 0: a segment of whole
+// blocks for one shard of a multi-GPU job (no frame byte).
 int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
         void *d_len, int hdr, void *stream) {
   if (!c || !d_in || !d_out || !d_len) return LZ4R_ERR_ARG;
   if (hdr && n < (size_t)kBlk) return LZ4R_ERR_TOO_SMALL;
-  if (n == 0) return LZ4R_ERR_ARG;
+  if (n == 0 || n > kMaxInput) return LZ4R_ERR_ARG;
   const size_t nb = (n + kBlk - 1) / kBlk;
+  const size_t nchunks = (nb + kChunk - 1) / kChunk;
   int rc = ensure_scratch(c, nb);
   if (rc != LZ4R_OK) return rc;
-  if (nb > 0xffffffffULL || n > (1ull << 37)) return LZ4R_ERR_ARG;
   static_assert(kPart % kGT == 0, "partials hold whole groups");
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool timed = c->timing;
+  if (timed && (rc = ensure_events(c, nchunks)) != LZ4R_OK) return rc;
   c->timed_call = timed;
+  c->timed_chunks = nchunks;
   if (timed) (void)hipEventRecord(c->ev_a, s);
-  // one tile per workgroup: the hardware dispatcher balances the uneven
-  // per-tile cost (a static grid-stride split leaves a tail; measured slower
-  // also with the next block prefetched into registers)
-  static const unsigned extra_lds = getenv("LZ4R_EXTRA_LDS") ? (unsigned)atoi(getenv("LZ4R_EXTRA_LDS")) : 0u;
-  const uint32_t per = (uint32_t)((nb + 7) / 8);       // blocks per XCD slice
-  hipLaunchKernelGGL(lz4_tiles, dim3(8 * per), dim3(64), extra_lds, s,
-                     static_cast<const uint8_t *>(d_in), (uint32_t)nb, per,
-                     (uint32_t)(n - (nb - 1) * kBlk), c->slots, c->tsz, c->bsizes);
-  if (timed) (void)hipEventRecord(c->ev_b, s);
-  const size_t nparts = (nb + kPart - 1) / kPart;
-  hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)nparts), dim3(256), 0, s, c->tsz, nb,
-                     (size_t)0, c->gsum, c->part);
-  hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part, nparts,
-                     (uint64_t)hdr, 1, static_cast<uint64_t *>(d_len));
-  const size_t ngroups = (nb + kGT - 1) / kGT;
-  hipLaunchKernelGGL(lz4_gather, dim3((unsigned)(ngroups * kGSplit)), dim3(256), 0, s, c->slots,
-                     c->tsz, nb, (size_t)0, c->gsum, c->part, static_cast<uint8_t *>(d_out),
-                     (uint64_t)cap, hdr, (uint64_t)nb);
+  const uint8_t *in = static_cast<const uint8_t *>(d_in);
+  for (size_t k = 0; k < nchunks; ++k) {
+    const size_t b0 = k * kChunk;                      // first block of the chunk
+    const size_t nbc = std::min(kChunk, nb - b0);
+    const size_t b1 = b0 + nbc;
+    const uint32_t last_n = (uint32_t)(b1 == nb ? n - (nb - 1) * kBlk : kBlk);
+    // one block per workgroup: the hardware dispatcher balances the uneven
+    // per-block cost (a static grid-stride split leaves a tail; measured
+    // slower also with the next block prefetched into registers)
+    const uint32_t per = (uint32_t)((nbc + 7) / 8);    // blocks per XCD slice
+    if (timed) (void)hipEventRecord(c->ev_tiles[2 * k], s);
+    hipLaunchKernelGGL(lz4_tiles, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk, (uint32_t)nbc,
+                       per, last_n, c->slots, c->tsz + b0, c->bsizes + b0);
+    if (timed) (void)hipEventRecord(c->ev_tiles[2 * k + 1], s);
+    const size_t p0 = b0 / kPart, np = (nbc + kPart - 1) / kPart;
+    hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)np), dim3(256), 0, s, c->tsz, b1, p0,
+                       c->gsum, c->part);
+    hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part + p0, np,
+                       (uint64_t)hdr, k == 0 ? 1 : 0, static_cast<uint64_t *>(d_len));
+    const size_t g0 = b0 / kGT, ng = (nbc + kGT - 1) / kGT;
+    hipLaunchKernelGGL(lz4_gather, dim3((unsigned)(ng * kGSplit)), dim3(256), 0, s, c->slots,
+                       b0, c->tsz, b1, g0, c->gsum, c->part, static_cast<uint8_t *>(d_out),
+                       (uint64_t)cap, hdr, (uint64_t)nb, c->boff);
+  }
   if (timed) (void)hipEventRecord(c->ev_c, s);
   c->last_nb = nb;
   const hipError_t e = hipGetLastError();
@@ -930,25 +967,16 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
 
 extern "C" {
 
-
 int lz4r_ctx_create(lz4r_ctx **out) {
   if (!out) return LZ4R_ERR_ARG;
   lz4r_ctx *c = new (std::nothrow) lz4r_ctx();
   if (!c) return LZ4R_ERR_NOMEM;
-  int cus = 0, occ = 0;
   if (hipGetDevice(&c->device) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) !=
-          hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lz4_tiles, 64, 0) != hipSuccess ||
-      cus <= 0 || occ <= 0 ||
       hipMalloc(&c->len, sizeof(uint64_t)) != hipSuccess ||
-      hipEventCreate(&c->ev_a) != hipSuccess || hipEventCreate(&c->ev_b) != hipSuccess ||
-      hipEventCreate(&c->ev_c) != hipSuccess) {
+      hipEventCreate(&c->ev_a) != hipSuccess || hipEventCreate(&c->ev_c) != hipSuccess) {
     lz4r_ctx_destroy(c);
     return LZ4R_ERR_HIP;
   }
-  // one resident wave per LDS/VGPR slot; tiles are taken grid-stride
-  c->max_grid = (unsigned)(occ * cus);
   *out = c;
   return LZ4R_OK;
 }
@@ -958,8 +986,8 @@ void lz4r_ctx_destroy(lz4r_ctx *c) {
   free_scratch(c);
   (void)hipFree(c->len);
   if (c->ev_a) (void)hipEventDestroy(c->ev_a);
-  if (c->ev_b) (void)hipEventDestroy(c->ev_b);
   if (c->ev_c) (void)hipEventDestroy(c->ev_c);
+  for (hipEvent_t e : c->ev_tiles) (void)hipEventDestroy(e);
   delete c;
 }
 
@@ -973,7 +1001,19 @@ int lz4r_compress_async(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, si
 }
 
 int lz4r_compress_segment_async(lz4r_ctx *c, const void *d_in, size_t n, void *d_out,
-                                size_t cap, void *d_len, void *stream) {
+                                size_t cap, void *d_len, int final_shard, void *stream) {
+  if (!c || !d_len) return LZ4R_ERR_ARG;
+  // a non-final shard must end on the 300-B grid, or the blocks after it
+  // (and so the concatenated stream) would differ from the single-GPU one
+  if (!final_shard && n % kBlk != 0) return LZ4R_ERR_ARG;
+  if (n == 0) {                      // an empty shard (more ranks than blocks)
+    c->last_nb = 0;
+    c->timed_call = false;
+    return hipMemsetAsync(d_len, 0, sizeof(uint64_t), static_cast<hipStream_t>(stream)) ==
+                   hipSuccess
+               ? LZ4R_OK
+               : LZ4R_ERR_HIP;
+  }
   return run(c, d_in, n, d_out, cap, d_len, 0, stream);
 }
 
@@ -996,6 +1036,7 @@ int lz4r_compress_device(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, s
 
 int lz4r_copy_block_sizes(const lz4r_ctx *c, void *dst, size_t count, void *stream) {
   if (!c || !dst || count > c->last_nb) return LZ4R_ERR_ARG;
+  if (count == 0) return LZ4R_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (hipMemcpyAsync(dst, c->bsizes, count * sizeof(uint16_t), hipMemcpyDefault, s) !=
           hipSuccess ||
@@ -1006,17 +1047,19 @@ int lz4r_copy_block_sizes(const lz4r_ctx *c, void *dst, size_t count, void *stre
 
 int lz4r_copy_block_offsets(const lz4r_ctx *c, void *dst, size_t count, void *stream) {
   if (!c || !dst || count > c->last_nb) return LZ4R_ERR_ARG;
-  std::vector<uint16_t> sz(count);
-  std::vector<uint64_t> off(count);
-  int rc = lz4r_copy_block_sizes(c, sz.data(), count, stream);
-  if (rc != LZ4R_OK) return rc;
-  uint64_t acc = 0;
-  for (size_t i = 0; i < count; ++i) {
-    off[i] = acc;
-    acc += sz[i];
-  }
-  if (hipMemcpy(dst, off.data(), count * sizeof(uint64_t), hipMemcpyDefault) != hipSuccess)
+  if (count == 0) return LZ4R_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipMemcpyAsync(dst, c->boff, count * sizeof(uint64_t), hipMemcpyDefault, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
     return LZ4R_ERR_HIP;
+  return LZ4R_OK;
+}
+
+int lz4r_block_offsets_device(const lz4r_ctx *c, const void **d_offsets, size_t *count) {
+  if (!c || !d_offsets || !count) return LZ4R_ERR_ARG;
+  *d_offsets = c->boff;
+  *count = c->last_nb;
   return LZ4R_OK;
 }
 
@@ -1057,9 +1100,13 @@ int lz4r_last_timing(lz4r_ctx *c, float *ms_call, float *ms_match) {
   if (!c || !c->timed_call) return LZ4R_ERR_ARG;
   if (hipEventSynchronize(c->ev_c) != hipSuccess) return LZ4R_ERR_HIP;
   float a = 0.f, b = 0.f;
-  if (hipEventElapsedTime(&a, c->ev_a, c->ev_c) != hipSuccess ||
-      hipEventElapsedTime(&b, c->ev_a, c->ev_b) != hipSuccess)
-    return LZ4R_ERR_HIP;
+  if (hipEventElapsedTime(&a, c->ev_a, c->ev_c) != hipSuccess) return LZ4R_ERR_HIP;
+  for (size_t k = 0; k < c->timed_chunks; ++k) {
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, c->ev_tiles[2 * k], c->ev_tiles[2 * k + 1]) != hipSuccess)
+      return LZ4R_ERR_HIP;
+    b += t;
+  }
   if (ms_call) *ms_call = a;
   if (ms_match) *ms_match = b;
   return LZ4R_OK;

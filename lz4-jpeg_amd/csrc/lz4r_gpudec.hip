@@ -353,8 +353,11 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
           pfv[t] = *(q < qe ? q : q0 - kPfS);          // one byte: never past the stream
         }
       }
-      // a read reaches at most kInMax + 32 bytes past the wave's first block
-      if (1 + boff[b0] + (size_t)(kLanes + 1) * kInMax + 64 <= in_len)
+      // a lane's reads reach at most 32 bytes past its block (<= kInMax bytes):
+      // unchecked loads only when that stays inside the stream, decided per
+      // lane from its own offsets (caller-supplied offsets need not be
+      // monotone; only the stream's last few blocks take the checked path)
+      if (beg + (size_t)kInMax + 64 <= in_len)
         q = decode_block(Bytes<false>{in + beg, in_len - beg}, (int)(end - beg), last, o);
       else
         q = decode_block(Bytes<true>{in + beg, in_len - beg}, (int)(end - beg), last, o);

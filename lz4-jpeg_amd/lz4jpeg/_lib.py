@@ -23,9 +23,10 @@ SIGNATURES = [
     ("lz4r_nblocks", _c_size, [_c_size]),
     ("lz4r_compress_device", _i, [_vp, _vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size), _vp]),
     ("lz4r_compress_async", _i, [_vp, _vp, _c_size, _vp, _c_size, _vp, _vp]),
-    ("lz4r_compress_segment_async", _i, [_vp, _vp, _c_size, _vp, _c_size, _vp, _vp]),
+    ("lz4r_compress_segment_async", _i, [_vp, _vp, _c_size, _vp, _c_size, _vp, _i, _vp]),
     ("lz4r_copy_block_sizes", _i, [_vp, _vp, _c_size, _vp]),
     ("lz4r_copy_block_offsets", _i, [_vp, _vp, _c_size, _vp]),
+    ("lz4r_block_offsets_device", _i, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_c_size)]),
     ("lz4r_compress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
     ("lz4r_decompress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
     ("lz4r_decompress_device", _i, [_vp, _c_size, _vp, _c_size, _vp, _c_size, _vp, _vp]),
@@ -51,6 +52,14 @@ SIGNATURES = [
     ("lz4jpeg_rand_rgba", None, [ctypes.c_uint, _i, _i, _vp]),
     ("lz4jpeg_random_passages", _c_size, [_vp, _c_size, ctypes.c_uint, _c_size, _c_size, _c_size,
                                          _vp]),
+    ("lz4jpeg_rand_rgba_stream", None, [ctypes.c_uint, ctypes.c_uint64, _c_size, _vp]),
+    ("lz4jpeg_rand_states", None, [ctypes.c_uint, ctypes.c_uint64, ctypes.c_uint64, _c_size,
+                                   _vp]),
+    ("lz4jpeg_passage_starts", _c_size, [_c_size, ctypes.c_uint, _c_size, ctypes.c_uint64,
+                                         _c_size, _vp]),
+    ("lz4jpeg_rand_rgba_device", _i, [ctypes.c_uint, ctypes.c_uint64, _c_size, _vp, _vp]),
+    ("lz4jpeg_random_passages_device", _i, [_vp, _c_size, ctypes.c_uint, _c_size,
+                                            ctypes.c_uint64, _c_size, _vp, _vp]),
     # lz4jpeg_compat.h (the reference's own function names, on the GPU path)
     ("lz4_encode", None, []),
     ("LZ4_decode", None, [ctypes.c_char_p, ctypes.c_char_p]),

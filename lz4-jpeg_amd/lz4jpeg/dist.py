@@ -90,14 +90,22 @@ def compress_sharded(local, n_total, compress_segment, dst=0, group=None):
     return gather_stream(seg, seg_len, nblocks(n_total), lens, offs, dst, group)
 
 
-def hip_segment_compressor(compressor, stream=None):
-    """compress_segment callable over the HIP path (lz4r_compress_segment_async)."""
+def hip_segment_compressor(compressor, final_shard, stream=None):
+    """compress_segment callable over the HIP path (lz4r_compress_segment_async).
+    `final_shard`: this rank holds the globally last block (the only shard
+    that may end short).  An empty shard (more ranks than blocks) gives
+    length 0 without a launch."""
     from .lz4 import compress_bound
 
     def run(local):
         n = local.numel()
+        if n == 0:
+            return torch.empty(1, dtype=torch.uint8, device=local.device), 0
         out = torch.empty(compress_bound(n), dtype=torch.uint8, device=local.device)
         d_len = torch.zeros(1, dtype=torch.int64, device=local.device)
-        compressor.compress_async(local, n, out, d_len, stream=stream, segment=True)
+        compressor.compress_async(local, n, out, d_len, stream=stream, segment=True,
+                                  final_shard=final_shard)
+        if stream is not None:
+            stream.synchronize()      # .item() below waits only for torch's current stream
         return out, int(d_len.item())
     return run

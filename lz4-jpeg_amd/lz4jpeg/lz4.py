@@ -82,15 +82,21 @@ class Compressor:
             _raise(rc, "lz4r_compress_device")
         return d_out, got.value
 
-    def compress_async(self, d_in, n, d_out, d_len, stream=None, segment=False):
+    def compress_async(self, d_in, n, d_out, d_len, stream=None, segment=False,
+                       final_shard=True):
         """Enqueue only; the uint64 length lands in d_len (1-element int64 tensor).
-        segment=True: whole blocks without the frame header (one shard)."""
-        fn = (_lib.lib().lz4r_compress_segment_async if segment
-              else _lib.lib().lz4r_compress_async)
-        rc = fn(self._h, ctypes.c_void_p(d_in.data_ptr()), n, ctypes.c_void_p(d_out.data_ptr()),
-                d_out.numel(), ctypes.c_void_p(d_len.data_ptr()), _stream_handle(stream))
+        segment=True: whole blocks without the frame header (one shard); a
+        non-final shard (final_shard=False) must be a multiple of 300 bytes."""
+        L = _lib.lib()
+        args = (self._h, ctypes.c_void_p(d_in.data_ptr()), n, ctypes.c_void_p(d_out.data_ptr()),
+                d_out.numel(), ctypes.c_void_p(d_len.data_ptr()))
+        if segment:
+            rc = L.lz4r_compress_segment_async(*args, 1 if final_shard else 0,
+                                               _stream_handle(stream))
+        else:
+            rc = L.lz4r_compress_async(*args, _stream_handle(stream))
         if rc != 0:
-            _raise(rc, "lz4r_compress_async")
+            _raise(rc, "lz4r_compress_segment_async" if segment else "lz4r_compress_async")
 
     def block_offsets(self, count, stream=None):
         """numpy uint64 array: the last call's first `count` per-block output
@@ -101,6 +107,16 @@ class Compressor:
         if rc != 0:
             _raise(rc, "lz4r_copy_block_offsets")
         return out
+
+    def block_offsets_device(self):
+        """(device pointer, count) of the last call's per-block offsets, as the
+        placement kernel wrote them (valid until the next call on this
+        context); lz4r_block_offsets_device."""
+        ptr, cnt = ctypes.c_void_p(), ctypes.c_size_t(0)
+        rc = _lib.lib().lz4r_block_offsets_device(self._h, ctypes.byref(ptr), ctypes.byref(cnt))
+        if rc != 0:
+            _raise(rc, "lz4r_block_offsets_device")
+        return ptr.value, cnt.value
 
     def set_timing(self, enable=True):
         """Record HIP events on the launch stream around each call and its
@@ -164,7 +180,8 @@ def decompress_device(d_stream, length, d_offsets, nb, out_cap, d_out=None, stre
                       check=True):
     """Block-parallel GPU decode (lz4r_decompress_device).  d_stream: uint8
     tensor holding the framed stream (first `length` bytes); d_offsets: int64
-    tensor of nb per-block offsets (Compressor.block_offsets).  Returns
+    tensor of nb per-block offsets (Compressor.block_offsets), or the raw
+    device pointer Compressor.block_offsets_device() returns.  Returns
     (d_out, decoded_length); raises Lz4Error(-6) naming the first malformed
     block.  check=False skips the result read-back (no host sync) and
     returns (d_out, None)."""
@@ -172,14 +189,17 @@ def decompress_device(d_stream, length, d_offsets, nb, out_cap, d_out=None, stre
     if d_out is None:
         d_out = torch.empty(max(out_cap, 1), dtype=torch.uint8, device=d_stream.device)
     res = torch.empty(2, dtype=torch.int64, device=d_stream.device)
+    offs = d_offsets if isinstance(d_offsets, int) else d_offsets.data_ptr()
     rc = _lib.lib().lz4r_decompress_device(
-        ctypes.c_void_p(d_stream.data_ptr()), length, ctypes.c_void_p(d_offsets.data_ptr()), nb,
+        ctypes.c_void_p(d_stream.data_ptr()), length, ctypes.c_void_p(offs), nb,
         ctypes.c_void_p(d_out.data_ptr()), out_cap, ctypes.c_void_p(res.data_ptr()),
         _stream_handle(stream))
     if rc != 0:
         _raise(rc, "lz4r_decompress_device")
     if not check:
         return d_out, None
+    if stream is not None:
+        stream.synchronize()          # the result is written on `stream`, not torch's current one
     n, bad = (int(x) for x in res.cpu().tolist())
     if bad != -1:
         raise Lz4Error(_lib.LZ4R_ERR_CORRUPT, f"lz4r_decompress_device: block {bad - 1}")

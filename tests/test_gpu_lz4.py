@@ -106,10 +106,46 @@ def test_segments_concatenate_to_stream(comp, oracle):
         d_in = torch.from_numpy(np.frombuffer(data[lo:hi], dtype=np.uint8).copy()).cuda()
         out = torch.empty(1 + ldist.nblocks(hi - lo) * 1152, dtype=torch.uint8, device="cuda")
         d_len = torch.zeros(1, dtype=torch.int64, device="cuda")
-        comp.compress_async(d_in, hi - lo, out, d_len, segment=True)
+        comp.compress_async(d_in, hi - lo, out, d_len, segment=True, final_shard=(r == 2))
         torch.cuda.synchronize()
         parts.append(out[:int(d_len.item())].cpu().numpy().tobytes())
     assert bytes([nb & 0xFF]) + b"".join(parts) == oracle.lz4_compress(data)
+
+
+def test_segment_contract_rejects_misaligned_nonfinal_shard(comp):
+    """Only the globally last shard may end in a short block (lz4r.h)."""
+    import torch
+    from lz4jpeg import lz4
+    d_in = torch.zeros(1000, dtype=torch.uint8, device="cuda")
+    out = torch.empty(4096, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(1, dtype=torch.int64, device="cuda")
+    with pytest.raises(lz4.Lz4Error) as ei:
+        comp.compress_async(d_in, 1000, out, d_len, segment=True, final_shard=False)
+    assert ei.value.code == -1
+    comp.compress_async(d_in, 900, out, d_len, segment=True, final_shard=False)
+    comp.compress_async(d_in, 1000, out, d_len, segment=True, final_shard=True)
+    d_len.fill_(123)
+    comp.compress_async(d_in, 0, out, d_len, segment=True, final_shard=True)   # empty shard
+    torch.cuda.synchronize()
+    assert int(d_len.item()) == 0
+
+
+def test_device_block_offsets_delimit_every_block(comp, oracle):
+    """The placement kernel's device offsets (lz4r_block_offsets_device) cut
+    the stream into exactly the oracle's per-block bytes."""
+    import torch
+    data = golden_inputs.lz4_input("metamorphosis_spaces")
+    d_in = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    d_out, length = comp.compress_device(d_in)
+    nb = (len(data) + 299) // 300
+    ptr, cnt = comp.block_offsets_device()
+    assert cnt == nb and ptr
+    offs = comp.block_offsets(nb).astype(np.int64)
+    stream = d_out[:length].cpu().numpy().tobytes()
+    ends = list(offs[1:]) + [length - 1]
+    buf = np.frombuffer(data, dtype=np.uint8)
+    for b in range(nb):
+        assert stream[1 + offs[b]:1 + ends[b]] == oracle.lz4_blocks(buf, b, b + 1), b
 
 
 def test_capacity_error_reports_need(comp):
