@@ -27,7 +27,8 @@ all: lib bin oracle tools
 
 lib: $(LIB)
 
-bin: $(BIN)/LZ4_seq $(BIN)/JPEG_seq $(BIN)/LZ4_seq.exe $(BIN)/JPEG_seq.exe
+bin: $(BIN)/LZ4_seq $(BIN)/JPEG_seq $(BIN)/LZ4_seq.exe $(BIN)/JPEG_seq.exe \
+     $(BIN)/LZ4_par $(BIN)/JPEG_par $(BIN)/LZ4_par.exe $(BIN)/JPEG_par.exe
 
 $(CSRC)/jpeg_tables.h: $(CSRC)/gen_jpeg_tables.py
 	python3 $< > $@
@@ -52,11 +53,35 @@ $(BIN)/JPEG_seq: $(B)/jpeg_seq.o $(B)/png_io.o $(OBJS)
 	@mkdir -p $(BIN)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -lz
 
+# the parallel drivers' executables (Experiment/*_parallel_experiment.c)
+$(B)/lz4_par.o: $(HOST)/lz4_seq.c $(HDRS)
+	@mkdir -p $(B)
+	$(CC) $(CFLAGS_HOST) -DLZ4_PAR -c $< -o $@
+
+$(BIN)/LZ4_par: $(B)/lz4_par.o $(OBJS)
+	@mkdir -p $(BIN)
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^
+
+$(BIN)/JPEG_par: $(BIN)/JPEG_seq
+	cp $< $@
+
 $(BIN)/%.exe: $(BIN)/%
 	cp $< $@
 
 oracle:
 	$(MAKE) -C oracle
+
+# ASan + UBSan build of the host C (no HIP) and the oracle restatements,
+# driven by tests/sanitize/sanitize_main.c; tests/test_sanitize.py
+SAN_SRC := tests/sanitize/sanitize_main.c $(HOST)/lz4r_decode.c $(HOST)/png_io.c \
+           $(HOST)/synth.c oracle/lz4_oracle.c oracle/jpeg_oracle.c oracle/jpeg_entropy_oracle.c
+sanitize: build/sanitize_main
+
+build/sanitize_main: $(SAN_SRC) include/lz4r.h include/lz4jpeg_synth.h
+	@mkdir -p build
+	$(CC) -O1 -g -std=gnu11 -ffp-contract=off -fno-omit-frame-pointer \
+	  -fsanitize=address,undefined -fno-sanitize-recover=all \
+	  -o $@ $(SAN_SRC) -lz -lm -lpthread
 
 # micro-benchmarks: SIMD issue rates (tools/issue.sh) and LDS access costs
 tools: tools/variants/valu_rate tools/variants/lds_rate
@@ -70,7 +95,7 @@ tools/variants/lds_rate: tools/lds_rate.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -Wno-unused-result -o $@ $<
 
 clean:
-	rm -rf $(B) $(BIN) $(LIB)
+	rm -rf $(B) $(BIN) $(LIB) build
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib bin oracle tools clean
+.PHONY: all lib bin oracle tools sanitize clean

@@ -90,6 +90,15 @@ int lz4r_compress_segment_async(lz4r_ctx *ctx, const void *d_in, size_t n,
                                 void *d_out, size_t cap, void *d_out_len,
                                 int final_shard, void *stream);
 
+/* find_longest_match (LZ4.c:290-323) at every position of every 300-byte
+ * block of the n bytes at d_in, in one launch, asynchronous on `stream`:
+ * d_matches[300 b + p] (uint32, n entries, device) = len | dist << 16 for
+ * the longest match at p of block b (the earliest source among equals,
+ * LZ4.c:307; matches clamped at the block end), or 0 when len < 4
+ * (MIN_MATCH_LENGTH).  len is not truncated: the reference's uint8_t return
+ * value is len & 0xFF. */
+int lz4r_block_matches_device(const void *d_in, size_t n, void *d_matches, void *stream);
+
 /* After a compress call: copy the encoded byte count (uint16) of each of the
  * first `count` blocks of the last call to `dst` (host or device memory),
  * then synchronise `stream`.  Block b's bytes start at sum(sizes[0..b)) after

@@ -240,9 +240,12 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("" ::: "memory");
 }
 
-// Encode block `k` of the tile (n bytes at S.buf[kInOff + 300k]) into
-// S.buf[obase ...]; returns the bytes written.
-__device__ __forceinline__ int encode_block(TileLds &S, int n) {
+// Encode the staged block (n bytes at S.buf[kInOff]) into S.buf[0 ...];
+// returns the bytes written.  kMatchesOnly: stop after the best-match scan
+// and store every position's find_longest_match result to mout instead
+// (lz4r_block_matches_device).
+template <bool kMatchesOnly>
+__device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restrict__ mout) {
   const int lane = threadIdx.x;
   constexpr int base = kInOff;
   constexpr int obase = 0;
@@ -405,6 +408,17 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n) {
     const uint32_t excl = dpp<0x138, 0xf, 0xf>(incl);     // wave_shr:1, lane 0 gets 0
 #pragma unroll
     for (int r = 0; r < 5; ++r) v[r] = max(v[r], excl);
+  }
+  if constexpr (kMatchesOnly) {
+    // find_longest_match (LZ4.c:290-323) at every p: len | dist << 16, both 0
+    // below MIN_MATCH_LENGTH (the uint8_t truncation is the caller's)
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int p = p0 + r;
+      const int len = (int)(v[r] >> 9) - p;
+      if (p < n) mout[p] = len >= 4 ? (uint32_t)len | ((v[r] & 511u) << 16) : 0u;
+    }
+    return 0;
   }
   uint32_t mrec[5];
   int f[6];                       // f[r] = first matchable position >= p0 + r
@@ -642,7 +656,7 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   }
   wave_sync();
 
-  const int W = encode_block(S, n);
+  const int W = encode_block<false>(S, n, nullptr);
   // the block's bytes -> its 16-B aligned slot (<= 35 chunks: one round)
   uint4 *dst = reinterpret_cast<uint4 *>(slots + (size_t)t * kSlot);
   if (lane < ((W + 15) >> 4)) dst[lane] = reinterpret_cast<const uint4 *>(S.buf)[lane];
@@ -650,6 +664,22 @@ __global__ __launch_bounds__(64) void lz4_tiles(
     usz[t] = (uint32_t)W;
     bsizes[t] = (uint16_t)W;
   }
+}
+
+// Per-position longest matches of every block (the batch form of
+// find_longest_match): the same staging and match finder as lz4_tiles.
+__global__ __launch_bounds__(64) void lz4_matches(const uint8_t *__restrict__ in, uint32_t nb,
+                                                   uint32_t last_n, uint32_t *__restrict__ mout) {
+  __shared__ TileLds S;
+  const int lane = threadIdx.x;
+  const uint32_t t = blockIdx.x;
+  if (t >= nb) return;
+  const int n = t == nb - 1 ? (int)last_n : kBlk;
+  const uint8_t *src = in + (size_t)t * kBlk;
+  for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
+  if (lane < 16) S.buf[kInOff + n + lane] = 0;
+  wave_sync();
+  encode_block<true>(S, n, mout + (size_t)t * kBlk);
 }
 
 // ---- placement: exclusive scan of tile sizes, then gather -----------------
@@ -1032,6 +1062,17 @@ int lz4r_compress_device(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, s
   }
   *out_len = (size_t)need;
   return need > cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
+}
+
+int lz4r_block_matches_device(const void *d_in, size_t n, void *d_matches, void *stream) {
+  if (!d_in || !d_matches || n == 0) return LZ4R_ERR_ARG;
+  const size_t nb = (n + kBlk - 1) / kBlk;
+  if (nb > 0x7fffffffULL) return LZ4R_ERR_ARG;
+  hipLaunchKernelGGL(lz4_matches, dim3((unsigned)nb), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint8_t *>(d_in),
+                     (uint32_t)nb, (uint32_t)(n - (nb - 1) * kBlk),
+                     static_cast<uint32_t *>(d_matches));
+  return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
 }
 
 int lz4r_copy_block_sizes(const lz4r_ctx *c, void *dst, size_t count, void *stream) {

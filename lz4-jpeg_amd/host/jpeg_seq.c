@@ -1,6 +1,10 @@
 /*
- * JPEG_seq -- drop-in for the reference's JPEG_seq.exe
- * (Algorithms/sequential/JPEG/JPEG.c main, :1099-1460) on the MI355X path.
+ * JPEG_seq / JPEG_par -- drop-ins for the reference's JPEG_seq.exe
+ * (Algorithms/sequential/JPEG/JPEG.c main, :1099-1460) and JPEG_par.exe
+ * (spawned by Experiment/JPEG_parallel_experiment.c:99 system("JPEG_par.exe");
+ * the committed JPEG_par.exe reads and writes the same files as JPEG_seq.exe
+ * and computes the same tiles, one Win32 thread per 8x8 block) on the MI355X
+ * path: one program, installed under both names.
  *
  * File contract (run from Experiment/, JPEG_sequential_experiment.c:99):
  *   reads  ../Assets/Images/rand_8X8.png            (JPEG.c:9, :1102)

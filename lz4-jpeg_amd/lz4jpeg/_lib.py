@@ -27,6 +27,7 @@ SIGNATURES = [
     ("lz4r_copy_block_sizes", _i, [_vp, _vp, _c_size, _vp]),
     ("lz4r_copy_block_offsets", _i, [_vp, _vp, _c_size, _vp]),
     ("lz4r_block_offsets_device", _i, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_c_size)]),
+    ("lz4r_block_matches_device", _i, [_vp, _c_size, _vp, _vp]),
     ("lz4r_compress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
     ("lz4r_decompress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
     ("lz4r_decompress_device", _i, [_vp, _c_size, _vp, _c_size, _vp, _c_size, _vp, _vp]),
@@ -62,6 +63,9 @@ SIGNATURES = [
                                             ctypes.c_uint64, _c_size, _vp, _vp]),
     # lz4jpeg_compat.h (the reference's own function names, on the GPU path)
     ("lz4_encode", None, []),
+    ("find_longest_match", ctypes.c_uint8, [_vp, _c_size, ctypes.POINTER(ctypes.c_uint16)]),
+    ("block_encode", None, [_vp, _c_size, _vp, _vp, _vp, _vp]),
+    ("write_output", None, [_vp, _vp]),
     ("LZ4_decode", None, [ctypes.c_char_p, ctypes.c_char_p]),
     ("discrete_cosine_transform", None, [_vp, _c_size, _c_size, ctypes.POINTER(ctypes.POINTER(
         ctypes.c_double))]),

@@ -278,3 +278,39 @@ int ref_jpeg_entropy(const short *zz, int n, int *rle, int *rle_len, int *ncodes
     free(enc);
     return 0;
 }
+
+/* The reference's own visual PNGs (JPEG.c:1103-1123): original.png,
+ * luminance.png, rChrominance.png, bChrominance.png, written by its
+ * create_*_image functions through stb_image_write into
+ * OUTPUT_DIRECTORY ("../Output-Input/Images/", relative to the cwd -- run
+ * this from a scratch Experiment/ directory). */
+int ref_jpeg_visual_pngs(const unsigned char *rgba, int w, int h)
+{
+    ImageData img;
+    img.width = w;
+    img.height = h;
+    img.pixel_count = (size_t)w * h;
+    img.pixels = malloc(h * sizeof(Pixel *));
+    for (int y = 0; y < h; y++) {
+        img.pixels[y] = malloc(w * sizeof(Pixel));
+        for (int x = 0; x < w; x++) {
+            const unsigned char *p = rgba + ((size_t)y * w + x) * 4;
+            img.pixels[y][x].r = p[0];
+            img.pixels[y][x].g = p[1];
+            img.pixels[y][x].b = p[2];
+            img.pixels[y][x].a = p[3];
+        }
+    }
+    uint8_t **lum, **cr, **cb;
+    create_png_image("original.png", w, h, img.pixels);
+    build_luminance_matrix(img, &lum);
+    create_luminance_image("luminance.png", lum, img);
+    build_rChrominance_matrix(img, &cr);
+    create_rChrominance_image("rChrominance.png", cr, img);
+    build_bChrominance_matrix(img, &cb);
+    create_bChrominance_image("bChrominance.png", cb, img);
+    for (int y = 0; y < h; y++) { free(lum[y]); free(cr[y]); free(cb[y]); }
+    free(lum); free(cr); free(cb);
+    free_pixels(img.pixels, h);
+    return 0;
+}

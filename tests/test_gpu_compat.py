@@ -79,3 +79,93 @@ def test_lz4_encode_decode_file_contract(gpu, oracle, tmp_path, monkeypatch):
     assert comp == oracle.lz4_compress(data)
     L.LZ4_decode(b"../Output-Input/out/compressed.bin", b"../Output-Input/log/encoding_log.txt")
     assert (tmp_path / "Output-Input/out/uncompressed.txt").read_bytes() == data
+
+
+# ---- LZ4 per-block API: find_longest_match / block_encode / write_output ----
+class LZ4Sequence(ctypes.Structure):          # LZ4.c:30-38
+    _fields_ = [("token", ctypes.c_uint8), ("byte_size", ctypes.c_size_t),
+                ("literals", ctypes.c_void_p), ("literals_count", ctypes.c_size_t),
+                ("match_offset", ctypes.c_uint16), ("match_length", ctypes.c_size_t)]
+
+
+class LZ4Block(ctypes.Structure):             # LZ4.c:40-46
+    _fields_ = [("token", ctypes.c_uint8), ("byte_size", ctypes.c_size_t),
+                ("sequences_count", ctypes.c_size_t),
+                ("sequences", ctypes.POINTER(LZ4Sequence))]
+
+
+class LZ4Frame(ctypes.Structure):             # LZ4.c:48-52
+    _fields_ = [("blocks", ctypes.c_size_t), ("frame_blocks", ctypes.POINTER(LZ4Block))]
+
+
+def _libc():
+    c = ctypes.CDLL(None)
+    c.fopen.restype = ctypes.c_void_p
+    c.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    c.fclose.argtypes = [ctypes.c_void_p]
+    return c
+
+
+def _reference_loop(data, path):
+    """lz4_encode's block loop (LZ4.c:707-721) + write_output (:427-441),
+    through the C ABI."""
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    frame = LZ4Frame(0, None)
+    nb = (len(data) + 299) // 300
+    blocks = []
+    for i in range(nb):
+        blk = LZ4Block()
+        n = min(300, len(data) - 300 * i)
+        L.block_encode(ctypes.addressof(buf) + 300 * i, n, ctypes.byref(blk), None, None,
+                       ctypes.byref(frame))
+        blocks.append((blk.token, blk.byte_size, blk.sequences_count))
+    assert frame.blocks == nb
+    c = _libc()
+    f = c.fopen(str(path).encode(), b"wb")
+    L.write_output(ctypes.byref(frame), f)
+    c.fclose(f)
+    assert frame.blocks == 0
+    return open(path, "rb").read(), blocks
+
+
+@pytest.mark.parametrize("name", ["file:lz4_input.txt", "text_10000", "metamorphosis_spaces",
+                                  "m_eq_1", "m_eq_2", "m_eq_3", "len_256", "lit_270", "lit_300",
+                                  "text_last_block_1", "zeros_900", "alphabet2_3000"])
+def test_block_encode_and_write_output_equal_the_oracle(gpu, oracle, tmp_path, name):
+    data = golden_inputs.lz4_input(name)
+    got, blocks = _reference_loop(data, tmp_path / "c.bin")
+    assert got == oracle.lz4_compress(data)
+    # the committed golden pair, byte for byte
+    if name == "file:lz4_input.txt":
+        ref = open(os.path.join(golden_inputs.GOLDEN, "lz4_input.compressed.bin"), "rb").read()
+        assert got == ref
+
+
+def test_find_longest_match_every_position(gpu, oracle):
+    """find_longest_match at every position of a 300-B block (the standalone
+    form: the 300 bytes at `input`) against a direct restatement of
+    LZ4.c:290-323 with the block-end clamp."""
+    L = _lib.lib()
+    rng = np.random.default_rng(5)
+    text = golden_inputs.lz4_input("metamorphosis_spaces")
+    for trial in range(4):
+        if trial < 2:
+            blk = text[300 * (7 + trial):300 * (8 + trial)]
+        else:
+            blk = bytes(rng.integers(97, 100, 300, dtype=np.uint8))   # {a,b,c}: long matches
+        buf = ctypes.create_string_buffer(blk, 300)
+        for p in range(300):
+            best, bd = 0, 0
+            for i in range(p):
+                l = 0
+                while p + l < 300 and l < 1024 and blk[i + l] == blk[p + l]:
+                    l += 1
+                if l > best:
+                    best, bd = l, p - i
+            d = ctypes.c_uint16(0)
+            m = L.find_longest_match(ctypes.addressof(buf), p, ctypes.byref(d))
+            if best >= 4:
+                assert (m, d.value) == (best & 0xFF, bd), (trial, p)
+            else:
+                assert m == 0, (trial, p)

@@ -1,8 +1,9 @@
-"""The drop-in executables (lz4-jpeg_amd/bin/LZ4_seq.exe, JPEG_seq.exe) honour
+"""The drop-in executables (lz4-jpeg_amd/bin/{LZ4,JPEG}_{seq,par}.exe) honour
 the reference's file contract: run from Experiment/ with the
-reference's relative paths, exit status 0, outputs bit-exact to the oracle.
-The reference's own unmodified benchmark drivers (compiled from
-Experiment/*_sequential_experiment.c into oracle/_ref) drive them end to end."""
+reference's relative paths, exit status 0, outputs bit-exact to the oracle,
+visual PNGs pixel-equal to the reference's own writers.  The reference's own
+unmodified benchmark drivers (compiled from Experiment/*_experiment.c into
+oracle/_ref) drive them end to end."""
 import json
 import os
 import shutil
@@ -133,3 +134,92 @@ def test_reference_jpeg_driver_runs_unchanged(tmp_path, oracle):
     img = pngdec.read(str(tmp_path / "Assets/Images/rand_8X8.png"))       # last image
     coef = np.fromfile(tmp_path / "Output-Input/Images/coefficients.bin", dtype="<i2")
     assert np.array_equal(coef, oracle.jpeg_encode(img))
+
+
+def _layout_par(tmp):
+    exp = layout(tmp)
+    for exe in ("LZ4_par.exe", "JPEG_par.exe"):
+        shutil.copy(os.path.join(BIN, exe), os.path.join(exp, exe))
+    return exp
+
+
+def test_lz4_par_file_contract(tmp_path, oracle):
+    exp = _layout_par(str(tmp_path))
+    data = golden_inputs.lz4_input("text_10000")
+    open(tmp_path / "Output-Input/input/input.txt", "wb").write(data)
+    r = run(exp, ["./LZ4_par.exe"])
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "Output-Input/out/compressed.bin").read_bytes() == oracle.lz4_compress(data)
+    assert (tmp_path / "Output-Input/out/uncompressed.txt").read_bytes() == data
+    assert b"Number of cores available:" in r.stdout        # parallel LZ4.c:1246
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "LZ4_parallel_experiment")),
+                    reason="reference drivers not built (no /root/reference at build time)")
+def test_reference_lz4_parallel_driver_runs_unchanged(tmp_path, oracle):
+    """Experiment/LZ4_parallel_experiment.c, unmodified: 10 runs of
+    popen("LZ4_par.exe 2>&1") on 350-B extracts, retrying until exit 0."""
+    exp = _layout_par(str(tmp_path))
+    r = run(exp, [os.path.join(REF, "LZ4_parallel_experiment")], timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    res = json.load(open(os.path.join(exp, "results", "LZ4_par.exe_execution_times.json")))
+    assert [e["text"] for e in res] == [350] and len(res[0]["execution_times_sec"]) == 10
+    assert r.stdout.count(b"[SUCCESS] LZ4 processing successful") == 10
+    data = (tmp_path / "Output-Input/input/input.txt").read_bytes()
+    assert (tmp_path / "Output-Input/out/compressed.bin").read_bytes() == oracle.lz4_compress(data)
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "JPEG_parallel_experiment")),
+                    reason="reference drivers not built (no /root/reference at build time)")
+def test_reference_jpeg_parallel_driver_runs_unchanged(tmp_path, oracle):
+    """Experiment/JPEG_parallel_experiment.c, unmodified: images 1x1 .. 2048x2048,
+    10 runs each, system("JPEG_par.exe"); every run must succeed."""
+    exp = _layout_par(str(tmp_path))
+    r = run(exp, [os.path.join(REF, "JPEG_parallel_experiment")], timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert b"[ERROR] JPEG processing failed" not in r.stdout
+    assert r.stdout.count(b"[SUCCESS] JPEG processing successful") == 120
+    res = json.load(open(os.path.join(exp, "results", "JPEG_par.exe_execution_times.json")))
+    assert [e["image_size"] for e in res] == [2 ** i for i in range(12)]
+    img = pngdec.read(str(tmp_path / "Assets/Images/rand_8X8.png"))       # last image
+    coef = np.fromfile(tmp_path / "Output-Input/Images/coefficients.bin", dtype="<i2")
+    assert np.array_equal(coef, oracle.jpeg_encode(img))
+
+
+_VISUAL_SCRIPT = r"""
+import ctypes, os, sys
+import numpy as np
+lib = ctypes.CDLL(sys.argv[1])
+lib.ref_jpeg_visual_pngs.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+w, h = int(sys.argv[3]), int(sys.argv[4])
+img = np.fromfile(sys.argv[2], dtype=np.uint8)
+os.chdir(sys.argv[5])                     # OUTPUT_DIRECTORY is ../Output-Input/Images/
+sys.exit(lib.ref_jpeg_visual_pngs(img.ctypes.data, w, h))
+"""
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "libref_jpeg.so")),
+                    reason="reference JPEG.c not built (no /root/reference at build time)")
+@pytest.mark.parametrize("w,h", [(64, 48), (37, 21)])
+def test_visual_pngs_equal_the_reference(tmp_path, oracle, w, h):
+    """original / luminance / rChrominance / bChrominance.png decode to the
+    pixels the reference's own create_*_image (JPEG.c:187-300, its
+    double -> uint8_t conversions included) writes for the same image."""
+    ours, ref = tmp_path / "ours", tmp_path / "ref"
+    exp = layout(str(ours))
+    layout(str(ref))
+    img = oracle.rand_image(w, h, seed=9)
+    pngdec.write(str(ours / "Assets/Images/rand_8X8.png"), img)
+    assert run(exp, ["./JPEG_seq.exe"]).returncode == 0
+    raw = tmp_path / "img.raw"
+    np.ascontiguousarray(img).tofile(raw)
+    import sys
+    r = subprocess.run([sys.executable, "-c", _VISUAL_SCRIPT, os.path.join(REF, "libref_jpeg.so"),
+                        str(raw), str(w), str(h), str(ref / "Experiment")],
+                       capture_output=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    for name in ("original.png", "luminance.png", "rChrominance.png", "bChrominance.png"):
+        a = pngdec.read(str(ours / "Output-Input/Images" / name))
+        b = pngdec.read(str(ref / "Output-Input/Images" / name))
+        assert np.array_equal(a, b), name
