@@ -68,24 +68,54 @@
 #ifndef LZ4R_VARIANT
 #define LZ4R_VARIANT 0
 #endif
+// LZ4R_PROF (tools builds only, like LZ4R_VARIANT): per-phase s_memtime
+// cycles of every wave summed into lz4r_prof[] (read by lz4r_prof_read).
+#ifdef LZ4R_PROF
+__device__ unsigned long long lz4r_prof_acc[16];
+#define PROF_DECL uint64_t prof_t = __builtin_amdgcn_s_memtime()
+#define PROF_MARK(k)                                                     \
+  do {                                                                   \
+    const uint64_t prof_n = __builtin_amdgcn_s_memtime();                \
+    if (threadIdx.x == 0) atomicAdd(&lz4r_prof_acc[k], prof_n - prof_t); \
+    prof_t = prof_n;                                                     \
+  } while (0)
+#else
+#define PROF_DECL
+#define PROF_MARK(k) \
+  do {               \
+  } while (0)
+#endif
 
 
 namespace {
 
 constexpr int kBlk = LZ4R_BLOCK;          // 300
-constexpr int kTileIn = kBlk;             // staged input bytes (one block)
 constexpr int kBlkOutMax = 560;           // >= 548: worst-case bytes of one block, 16-B multiple
-// LDS byte region: the block being encoded writes its bytes at buf[0 ..
-// kBlkOutMax); the tile's input sits at kInOff + 300k; then an over-read pad.
-constexpr int kInOff = kBlkOutMax;
-constexpr int kRegion = kInOff + kTileIn + 48;  // + over-read pad (lcp, 32-B copy reads)
-constexpr int kHB = 9;                    // hash bits: 512 buckets
+constexpr int kHB = 10;                   // hash bits: 1024 buckets
 constexpr int kH = 1 << kHB;
 constexpr int kArr = kBlk + 4;
 constexpr int kQ = kBlk;                 // walker ring (<= one live walker per entry)
 constexpr int kCand = 128;               // candidate list (drained when a pass could fill it)
 
-static_assert(kInOff % 16 == 0 && kBlk == 75 * 4, "dword staging: 75 dwords");
+// LDS of one wave (5,088 B: 32 waves per CU).  Byte offsets in TileLds::buf:
+//   [kInOff, +348)     the block (byte kInOff - 1 is read as blk[-1]) + an
+//                      over-read pad (lcp reads, 8-byte literal words)
+//   [kOutOff, +560)    the block's output bytes (emission)
+//   [kQOff, +1216)     chain walkers (q), or the slow walk's sequence starts (seq)
+//   [kCandOff, +512)   candidate pairs; run-start marks of the emission
+// and while the block is indexed, the 1024 u16 bucket heads overlay
+// [kHeadOff, +2048) = the output area, q and the front of cand, all of them
+// dead until the index is built.
+constexpr int kInOff = 16;
+constexpr int kOutOff = 368;
+constexpr int kQOff = kOutOff + kBlkOutMax;
+constexpr int kCandOff = kQOff + 4 * kArr;
+constexpr int kBufBytes = kCandOff + 4 * kCand;
+constexpr int kHeadOff = kOutOff;
+static_assert(kInOff + kBlk + 48 <= kOutOff && kOutOff % 16 == 0 && kInOff % 16 == 0 &&
+                  kBlk == 75 * 4,
+              "dword staging (75 dwords), 16-B aligned output chunks");
+static_assert(kHeadOff + 2 * kH <= kBufBytes, "heads overlay the dead regions");
 
 // scratch bytes per block slot (640-B line-aligned slots measured the same)
 constexpr int kSlot = 560;
@@ -93,22 +123,22 @@ static_assert(kSlot % 16 == 0 && kSlot >= kBlkOutMax && kBlkOutMax / 16 <= 64,
               "aligned slots, one store round");
 
 struct TileLds {
-  alignas(16) uint8_t buf[kRegion];
-  union {
-    uint32_t head[kH / 2];  // bucket -> 1 + last inserted position (0: empty), u16 pairs
-    uint32_t q[kQ];       // then: chain walkers, walker | next chain entry << 16
-    uint32_t seq[kArr];   // then: per sequence, cpos | end << 16
-  };
+  alignas(16) uint8_t buf[kBufBytes];
   union {
     uint32_t ent[kArr];   // per position: link | preceding byte << 9 | tag << 17
     uint32_t nm[kArr];    // then: first matchable position >= x (dwords: no sub-dword LDS access)
     uint32_t jt[kArr];    // then: succ, succ^2, succ^3 of a match start (9 bits each)
   };
   uint32_t rec[kArr];     // local(p) accumulator; then M | dist<<8 | succ<<17
-  uint32_t cand[kCand];   // candidate pairs p | j << 16 awaiting the lcp pass
+  // bucket -> 1 + last inserted position (0: empty), u16 pairs (index phase)
+  __device__ __forceinline__ uint32_t *head() { return reinterpret_cast<uint32_t *>(buf + kHeadOff); }
+  // chain walkers, walker | next chain entry << 16 (candidate phase)
+  __device__ __forceinline__ uint32_t *q() { return reinterpret_cast<uint32_t *>(buf + kQOff); }
+  // per sequence, its match start (slow walk only)
+  __device__ __forceinline__ uint32_t *seq() { return reinterpret_cast<uint32_t *>(buf + kQOff); }
+  // candidate pairs p | j << 16 awaiting the lcp pass; emission run marks
+  __device__ __forceinline__ uint32_t *cand() { return reinterpret_cast<uint32_t *>(buf + kCandOff); }
 };
-
-
 
 __device__ __forceinline__ uint32_t lds_off(const uint32_t *a) {
   typedef __attribute__((address_space(3))) const uint32_t lds_u32;
@@ -240,7 +270,7 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("" ::: "memory");
 }
 
-// Encode the staged block (n bytes at S.buf[kInOff]) into S.buf[0 ...];
+// Encode the staged block (n bytes at S.buf[kInOff]) into S.buf[kOutOff ...];
 // returns the bytes written.  kMatchesOnly: stop after the best-match scan
 // and store every position's find_longest_match result to mout instead
 // (lz4r_block_matches_device).
@@ -248,7 +278,7 @@ template <bool kMatchesOnly>
 __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restrict__ mout) {
   const int lane = threadIdx.x;
   constexpr int base = kInOff;
-  constexpr int obase = 0;
+  constexpr int obase = kOutOff;
 
   // ---- index: per-bucket chains of the 4-gram starts -----------------------
   // Position p swaps itself (+1) into its bucket's head and keeps the
@@ -259,13 +289,14 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   // Every unordered pair of a bucket is met once, by the later-inserted of
   // the two walking its chain; walkers that continue are re-queued, so each
   // pass over the queue is balanced over the lanes whatever the chain lengths.
+  PROF_DECL;
   const bool search = LZ4R_VARIANT != 1 && LZ4R_VARIANT != 2;
   const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
   constexpr int kHeadW = kH / 2;          // head dwords (u16 heads)
   static_assert(kHeadW % 256 == 0, "head reset: 16-B stores");
 #pragma unroll
   for (int i = 0; i < kHeadW / 256; ++i)  // empty heads (the previous block's queue)
-    reinterpret_cast<uint4 *>(S.head)[i * 64 + lane] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4 *>(S.head())[i * 64 + lane] = make_uint4(0, 0, 0, 0);
   // Blocked layout: lane l owns the five positions p0 .. p0 + 4, p0 = 5 l
   // (lanes 60..63 own none of a 300-B block).  One 12-byte window per lane
   // gives all five 4-gram keys and preceding bytes; the five head swaps go
@@ -296,7 +327,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       tg[r] = (key[r] * 2654435761u) >> 17;
       const uint32_t bk = tg[r] >> (15 - kHB);
       sh[r] = (bk & 1u) << 4;
-      adr[r] = lds_off(act ? &S.head[bk >> 1] : &S.cand[lane]);   // inactive: own dword
+      adr[r] = lds_off(act ? &S.head()[bk >> 1] : &S.rec[min(p, kArr - 1)]);   // inactive: own dword
       clr[r] = act ? 0xFFFFu << sh[r] : 0u;               // inactive: a no-op swap
       set[r] = act ? ((uint32_t)p + 1u) << sh[r] : 0u;
     }
@@ -313,9 +344,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       item[r] = act && o ? (uint32_t)p | (link << 16) : 0u;
     }
   }
+  PROF_MARK(0);                       // index
   wave_sync();                       // the heads are dead: the queue overlays them
   // queue the walkers lane-major: one wave scan of the per-lane counts
-  int qwr;                               // walkers queued (S.q[0 .. qwr))
+  int qwr;                               // walkers queued (S.q()[0 .. qwr))
   {
     int cnt = 0;
 #pragma unroll
@@ -327,12 +359,13 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     for (int r = 0; r < 5; ++r) {
       const bool walk = item[r] != 0u;
       // branch-free: lanes without a walker write their own dword of the idle cand list
-      *(walk ? &S.q[at] : &S.cand[lane]) = item[r];
+      *(walk ? &S.q()[at] : &S.cand()[lane]) = item[r];
       at += walk;
     }
   }
   wave_sync();
 
+  PROF_MARK(1);                       // walker queue
   // ---- candidates: walk the chains ------------------------------------------
   // A pair (j < p) of one bucket is a candidate when the tags agree and the
   // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]).  Candidates go to
@@ -344,7 +377,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     auto drain = [&]() {
       wave_sync();
       for (int i = lane; i < ncand && LZ4R_VARIANT != 4; i += 64) {
-        const uint32_t pr = S.cand[i];
+        const uint32_t pr = S.cand()[i];
         const int p = (int)(pr & 0xFFFFu), j = (int)(pr >> 16);
         const int l = lcp(S.buf, base + j, base + p, n - p);
         // (end, dist) as the best scan wants it: for one p the larger end is
@@ -368,7 +401,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       const uint64_t em = ~vm;
       const int idx = qrd + rank_below(em);
       const uint64_t nm_ = em & ballot(idx < qwr);
-      const uint32_t it = S.q[min(idx, kQ - 1)];
+      const uint32_t it = S.q()[min(idx, kQ - 1)];
       a = (int)sel_mask(nm_, it & 0xFFFFu, (uint32_t)a);
       b = (int)sel_mask(nm_, it >> 16, (uint32_t)b);
       vm |= nm_;
@@ -381,7 +414,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       const uint64_t cm =
           vm & ballot((x >> 17) == 0) & (ballot(j == 0) | ballot((x & (255u << 9)) != 0));
       const int sl = (int)sel_mask(cm, (uint32_t)(ncand + rank_below(cm)), (uint32_t)kTrash);
-      S.cand[sl] = (uint32_t)p | ((uint32_t)j << 16);
+      S.cand()[sl] = (uint32_t)p | ((uint32_t)j << 16);
       ncand += __popcll(cm);
       b = (int)(o & 511u);
       vm &= ballot(b != 511);
@@ -393,6 +426,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     if (ncand) drain();
   }
   wave_sync();
+  PROF_MARK(2);                       // candidates + lcp
   // ---- best(p) = prefix lexmax of (end, dist) -------------------------------
   // blocked: a running max over the lane's five positions, one wave scan of
   // the lane totals, the exclusive prefix folded back in
@@ -429,6 +463,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     mrec[r] = (uint32_t)M | ((v[r] & 511u) << 8);
   }
 
+  PROF_MARK(3);                       // best scan
   // ---- nm(x): first matchable position >= x, for x in [0, n] ---------------
   {
     int loc = 1 << 20;            // the lane's own first matchable position
@@ -476,6 +511,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   }
   wave_sync();
 
+  PROF_MARK(4);                       // nm + jump table
   // ---- greedy parse = walk over match starts (LZ4.c:516-583) ---------------
   // The walk is the serial part of the block: from c0 = nm(0), each step
   // reads the jump-table word of the last recorded start (three more starts)
@@ -499,23 +535,24 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   const bool slow = it > 64;
   int Sv_slow = 0;
   if (slow) {
-    if (lane == 0) S.seq[0] = (uint32_t)F0;
+    if (lane == 0) S.seq()[0] = (uint32_t)F0;
     Sv_slow = 1;
     for (c = F0; c < n;) {
       const uint32_t t = __builtin_amdgcn_readfirstlane(S.jt[c]);
       const int a = (int)(t & 511u), b = (int)((t >> 9) & 511u), d = (int)(t >> 18);
-      if (lane >= 1 && lane <= 3) S.seq[Sv_slow + lane - 1] = lane == 1 ? a : lane == 2 ? b : d;
+      if (lane >= 1 && lane <= 3) S.seq()[Sv_slow + lane - 1] = lane == 1 ? a : lane == 2 ? b : d;
       Sv_slow += (a < n) + (b < n) + (d < n);
       c = d;
     }
     wave_sync();
   }
+  PROF_MARK(5);                       // walk
   // ---- sequences: lane kk = sequence kk ------------------------------------
   // A round is 64 consecutive sequences; the match sequences are a prefix
   // (cpos < n), followed by the literal-only tail when the last match ends
   // before n (LZ4.c:585-612).  Rounds go on while a round is all matches.
   if (lane < kBlkOutMax / 16)          // the output area starts zeroed: bytes land by ds_or
-    reinterpret_cast<uint4 *>(S.buf)[lane] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4 *>(S.buf + obase)[lane] = make_uint4(0, 0, 0, 0);
   wave_sync();
   int nseq = 0;
   int ocar = 3;                      // block header: u8 nseq, u16 size
@@ -529,7 +566,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       const uint32_t w = (uint32_t)__shfl((int)seqv, i & 63, 64);
       cq = kk == 0 ? (uint32_t)F0 : (i < it ? (w >> (9 * f)) & 511u : (uint32_t)n);
     } else {
-      cq = kk < Sv_slow ? S.seq[kk] : (uint32_t)n;
+      cq = kk < Sv_slow ? S.seq()[kk] : (uint32_t)n;
     }
     const bool ism = (int)cq < n;                                  // ends with a match
     const uint64_t mm = ballot(ism);
@@ -586,10 +623,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       uint32_t carry = 0;                        // 1 + the last run owning a word so far
       for (int g0 = 0; g0 < C; g0 += 64) {
         wave_sync();
-        S.cand[lane] = 0u;                       // run-start marks of this round
-        if (cw > 0 && st >= g0 && st < g0 + 64) S.cand[st - g0] = (uint32_t)lane + 1u;
+        S.cand()[lane] = 0u;                       // run-start marks of this round
+        if (cw > 0 && st >= g0 && st < g0 + 64) S.cand()[st - g0] = (uint32_t)lane + 1u;
         wave_sync();                             // marks of other lanes: no forwarding
-        const uint32_t k1 = max(wave_incl_max(S.cand[lane]), carry);
+        const uint32_t k1 = max(wave_incl_max(S.cand()[lane]), carry);
         carry = lane63(k1);
         const int g = g0 + lane;
         const int k = (int)k1 - 1;               // the run owning word g
@@ -616,6 +653,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     nseq += (int)__popcll(ballot(act));
     if (nm_r < 64) break;
   }
+  PROF_MARK(6);                       // emission
   if (lane == 0) {                                                     // LZ4.c:417-419
     const int bsz = szsum + 3;
     S.buf[obase] = (uint8_t)nseq;
@@ -659,7 +697,7 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   const int W = encode_block<false>(S, n, nullptr);
   // the block's bytes -> its 16-B aligned slot (<= 35 chunks: one round)
   uint4 *dst = reinterpret_cast<uint4 *>(slots + (size_t)t * kSlot);
-  if (lane < ((W + 15) >> 4)) dst[lane] = reinterpret_cast<const uint4 *>(S.buf)[lane];
+  if (lane < ((W + 15) >> 4)) dst[lane] = reinterpret_cast<const uint4 *>(S.buf + kOutOff)[lane];
   if (lane == 0) {
     usz[t] = (uint32_t)W;
     bsizes[t] = (uint16_t)W;
@@ -996,6 +1034,20 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
 }  // namespace
 
 extern "C" {
+
+#ifdef LZ4R_PROF
+int lz4r_prof_read(unsigned long long *host16, int reset) {
+  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(lz4r_prof_acc), 16 * sizeof(unsigned long long)) !=
+      hipSuccess)
+    return LZ4R_ERR_HIP;
+  if (reset) {
+    static const unsigned long long zero[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(lz4r_prof_acc), zero, sizeof(zero)) != hipSuccess)
+      return LZ4R_ERR_HIP;
+  }
+  return LZ4R_OK;
+}
+#endif
 
 int lz4r_ctx_create(lz4r_ctx **out) {
   if (!out) return LZ4R_ERR_ARG;

@@ -1,5 +1,8 @@
-"""Run the LZ4 compressor a few times on the 1 GiB bench corpus (for profilers)."""
+"""Run the LZ4 compressor on the 1 GiB bench corpus (for profilers and A/B
+timing): `reps` calls after 3 warm-up calls; prints each call's (whole call,
+lz4_tiles) ms and, last, the medians."""
 import os
+import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -9,12 +12,20 @@ from lz4jpeg import lz4, synth  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 30
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-host = synth.random_passages(n, length=30000, seed=1)
-d_in = torch.from_numpy(host).cuda()
+warm = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+d_in = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+synth.random_passages_device(d_in, n, length=30000, seed=1)
 c = lz4.Compressor()
-d_out = torch.empty(lz4.compress_bound(n), dtype=torch.uint8, device="cuda")
+d_out = torch.empty(n + n // 8 + (1 << 20), dtype=torch.uint8, device="cuda")
+for _ in range(warm):
+    c.compress_device(d_in, n, d_out)
 c.set_timing(True)
+calls, tiles = [], []
 for _ in range(reps):
     _, got = c.compress_device(d_in, n, d_out)
-    print("len", got, "ms", c.last_timing(), flush=True)
+    a, b = c.last_timing()
+    calls.append(a)
+    tiles.append(b)
+    print("len", got, "ms", (a, b), flush=True)
+print(f"median call {statistics.median(calls):.4f} ms, lz4_tiles {statistics.median(tiles):.4f} ms")
 c.close()
