@@ -84,7 +84,9 @@ __global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
   __shared__ double ylds[kTiles * kYStride];
   __shared__ double crl[kTiles * kCStride];
   __shared__ double cbl[kTiles * kCStride];
-  __shared__ __attribute__((aligned(16))) int16_t olds[RAW ? 8 : kTiles * 128];
+  // the strip's int16 output is staged over the luma samples once every
+  // thread holds its coefficients in registers (34 KB of LDS: 4 WGs per CU)
+  int16_t *const olds = reinterpret_cast<int16_t *>(ylds);
 
   const int img = blockIdx.y;
   const int br = blockIdx.x / strips;
@@ -137,6 +139,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
 #pragma unroll
   for (int x = 0; x < 8; ++x) cx[x] = dC8[x][u];
 
+  int qy[8], qc[2][4];
   // ---- phase 2: luma DCT row u (JPEG.c:471-491 with W=H=8) -----------------
   {
     const double *yt = ylds + tile * kYStride;
@@ -159,8 +162,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
       if (RAW) {
         if (tile_ok) static_cast<double *>(out)[tile_g * 128 + u * 8 + v] = coef;
       } else {
-        const int q = (int)(coef / (double)dLQ[u * 8 + v]);      // JPEG.c:626-627
-        olds[tile * 128 + dZZ8[u * 8 + v]] = (int16_t)q;
+        qy[v] = (int)(coef / (double)dLQ[u * 8 + v]);            // JPEG.c:626-627
       }
     }
   }
@@ -188,13 +190,20 @@ __global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
         if (tile_ok)
           static_cast<double *>(out)[tile_g * 128 + 64 + ch * 32 + u * 4 + v] = coef;
       } else {
-        const int q = (int)(coef / (double)dCQ[u * 4 + v]);
-        olds[tile * 128 + 64 + ch * 32 + dZZ4[u * 4 + v]] = (int16_t)q;
+        qc[ch][v] = (int)(coef / (double)dCQ[u * 4 + v]);
       }
     }
   }
 
   if (RAW) return;
+  __syncthreads();                   // every thread is done reading the samples
+#pragma unroll
+  for (int v = 0; v < 8; ++v) olds[tile * 128 + dZZ8[u * 8 + v]] = (int16_t)qy[v];
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      olds[tile * 128 + 64 + ch * 32 + dZZ4[u * 4 + v]] = (int16_t)qc[ch][v];
   __syncthreads();
 
   // ---- phase 4: coalesced store of the strip's tiles -------------------------
