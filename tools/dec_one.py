@@ -1,11 +1,10 @@
 """Compress the bench corpus once, then run the GPU decoder a few times (for
-profilers).  LZ4R_DECODE_STAGE_BYTES=0 forces the global-memory path."""
+profilers), on the compressor's device-resident block offsets."""
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "lz4-jpeg_amd")]
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from lz4jpeg import lz4, synth  # noqa: E402
 
@@ -15,7 +14,7 @@ d_in = torch.from_numpy(synth.random_passages(n, length=30000, seed=1)).cuda()
 c = lz4.Compressor()
 d_stream, length = c.compress_device(d_in)
 nb = (n + 299) // 300
-d_offs = torch.from_numpy(c.block_offsets(nb).astype(np.int64)).cuda()
+d_offs, _ = c.block_offsets_device()          # written by the placement kernel
 d_out = torch.empty(n + 300, dtype=torch.uint8, device="cuda")
 for _ in range(reps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

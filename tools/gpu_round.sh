@@ -1,14 +1,17 @@
-# Round check on the GPU box: parity tests, bench line, kernel-trace profile,
-# HBM traffic PMC passes.
+# Round check on the GPU box: parity tests, the default bench line, a
+# kernel-trace profile of the same bench command, HBM traffic PMC passes and
+# the compressor's instruction-issue counts.  Everything under gpurun_out/round/.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t1.log 2>&1 && \
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/b1.json 2> gpurun_out/b1.err && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/p1.log 2>&1 && \
-bash tools/traffic.sh > gpurun_out/traffic.log 2>&1 && \
-bash tools/issue.sh > gpurun_out/issue.log 2>&1
+O=gpurun_out/round
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.log && \
+python3 tools/prof_summary.py $O/prof > $O/kernels.md && \
+bash tools/traffic.sh > $O/traffic.log 2>&1 && cp gpurun_out/traffic/traffic.json $O/traffic.json && \
+bash tools/issue.sh > $O/issue.log 2>&1 && cp gpurun_out/issue/issue.json $O/issue.json
 rc=$?
-tail -3 gpurun_out/t1.log; cat gpurun_out/b1.json
+tail -2 $O/tests.log; grep -E "^\[bench\]" $O/bench.err | tail -12; cat $O/kernels.md
 exit $rc
