@@ -5,15 +5,15 @@
 // in every block, greedily parses with an exhaustive longest-match search over
 // the whole block prefix (find_longest_match, LZ4.c:290-323; strict '>' so the
 // smallest i -- farthest offset -- wins ties; length truncated to uint8_t).
-// Blocks are independent; the compressor is one compute kernel plus a cheap
-// placement pass:
+// Blocks are independent; the compressor is one compute kernel, a scan and
+// an emission pass:
 //
 // lz4_tiles: workgroup = one wave = one 300-B block (5.1 KB of LDS, <= 64
 // VGPRs -> 8 waves per SIMD; occupancy is what this LDS- and issue-bound
 // kernel lives on).  Per block:
 //   stage    the block's 75 dwords -> LDS (the only read of the input).
 //   position-parallel, blocked (lane l owns p = 5 l .. 5 l + 4):
-//     index  per-bucket chains of the 4-gram starts by a 9-bit hash: p swaps
+//     index  per-bucket chains of the 4-gram starts by a 10-bit hash: p swaps
 //            itself into its bucket's u16 head (ds_mskor_rtn_b32 on a dword of
 //            two heads) and keeps the old head as its link;
 //            entry = link | preceding byte << 9 | tag << 17.
@@ -35,21 +35,28 @@
 //            the greedy parse (LZ4.c:516-583) is the walk c0 = nm(0),
 //            c_{k+1} = succ(c_k), three sequences per LDS round trip through
 //            the jump table succ | succ^2 | succ^3.
-//   emit     sequence k on lane k: one packed wave scan of the bytes written
-//            and the size fields, token / size / literal-extension / offset
-//            bytes (write_sequence, LZ4.c:365-413); the literal runs
-//            flattened over the lanes as aligned 8-byte words.  Every byte
-//            lands in the zeroed LDS output area by an aligned ds_or: a
-//            misaligned LDS access is replayed at ~1-2 cycles per lane.
-//   store    the block's bytes -> its 16-B aligned scratch slot (one round of
-//            16-B stores), its size -> usz (u32, for the scan) and bsizes (u16).
+//   records  sequence k on lane k: one packed wave scan of the bytes the block
+//            takes and of its size fields; record k = match start | M << 9 |
+//            dist << 17 (its literal run starts where sequence k - 1's match
+//            ends) -> the block's slot, after a header dword (sum of the size
+//            fields | sequence count << 16); the block's byte count -> usz
+//            (u32, for the scan) and bsizes (u16).
 // lz4_scan_reduce / lz4_scan_partials: exclusive scan of the block sizes.
-// lz4_gather: 32 blocks per workgroup: slots -> zeroed LDS image of the
-// output range (aligned ds_or of shifted chunks) -> aligned 16-B global stores.
+// lz4_emit: 32 blocks per workgroup of 8 waves, 4 blocks per wave.  The
+// blocks' input is staged in LDS, their records flattened over the lanes (one
+// round = 64 sequences of one or more blocks), and the bytes of write_block /
+// write_sequence (LZ4.c:365-425) land by aligned ds_or in a zeroed LDS image
+// of the output range -- header bytes from the sequence lanes, literal runs
+// flattened over the lanes as aligned 8-byte words -- which leaves as aligned
+// 16-B stores.  Splitting the emission off lz4_tiles (which is bound by
+// instruction issue, one block per wave) lets a round of lz4_emit serve
+// several blocks: lz4_tiles 3.44 -> 2.97 ms per GiB, and the slot round trip
+// shrinks from ~310 B of bytes to ~100 B of records per block.
 // No workgroup ever waits on another (a fused decoupled look-back ran the
 // waves in lock-step at the pace of the slowest block of each round).
-// HBM traffic per input byte: 1 B read + ~1.1 B written by lz4_tiles, and
-// ~1.1 B read + ~1.03 B written by lz4_gather (+6 B/block of block sizes).
+// HBM traffic per input byte: 1 B read + ~0.35 B of records written by
+// lz4_tiles; ~1 B of input + ~0.43 B of record heads read and ~1.03 B
+// written by lz4_emit (+14 B/block of sizes and offsets).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -100,9 +107,9 @@ constexpr int kCand = 128;               // candidate list (drained when a pass 
 // LDS of one wave (5,088 B: 32 waves per CU).  Byte offsets in TileLds::buf:
 //   [kInOff, +348)     the block (byte kInOff - 1 is read as blk[-1]) + an
 //                      over-read pad (lcp reads, 8-byte literal words)
-//   [kOutOff, +560)    the block's output bytes (emission)
+//   [kOutOff, +560)    (spare: the heads' overlay; lz4_emit writes the bytes)
 //   [kQOff, +1216)     chain walkers (q), or the slow walk's sequence starts (seq)
-//   [kCandOff, +512)   candidate pairs; run-start marks of the emission
+//   [kCandOff, +512)   candidate pairs
 // and while the block is indexed, the 1024 u16 bucket heads overlay
 // [kHeadOff, +2048) = the output area, q and the front of cand, all of them
 // dead until the index is built.
@@ -117,7 +124,7 @@ static_assert(kInOff + kBlk + 48 <= kOutOff && kOutOff % 16 == 0 && kInOff % 16 
               "dword staging (75 dwords), 16-B aligned output chunks");
 static_assert(kHeadOff + 2 * kH <= kBufBytes, "heads overlay the dead regions");
 
-// scratch bytes per block slot (640-B line-aligned slots measured the same)
+// scratch bytes per block slot: the header dword and <= 121 sequence records
 constexpr int kSlot = 560;
 static_assert(kSlot % 16 == 0 && kSlot >= kBlkOutMax && kBlkOutMax / 16 <= 64,
               "aligned slots, one store round");
@@ -136,7 +143,7 @@ struct TileLds {
   __device__ __forceinline__ uint32_t *q() { return reinterpret_cast<uint32_t *>(buf + kQOff); }
   // per sequence, its match start (slow walk only)
   __device__ __forceinline__ uint32_t *seq() { return reinterpret_cast<uint32_t *>(buf + kQOff); }
-  // candidate pairs p | j << 16 awaiting the lcp pass; emission run marks
+  // candidate pairs p | j << 16 awaiting the lcp pass
   __device__ __forceinline__ uint32_t *cand() { return reinterpret_cast<uint32_t *>(buf + kCandOff); }
 };
 
@@ -191,14 +198,6 @@ __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
     l += diff ? (int)at : 16;
   } while (!diff && l < limit);
   return l < limit ? l : limit;
-}
-
-// OR the (<= 4) bytes of v into the zeroed byte area at offset x: two
-// aligned dwords (ds_or_b32), never a misaligned access
-__device__ __forceinline__ void or_bytes(uint32_t *buf32, int x, uint32_t v) {
-  const uint64_t w = (uint64_t)v << (8 * (x & 3));
-  atomicOr(&buf32[x >> 2], (uint32_t)w);
-  atomicOr(&buf32[(x >> 2) + 1], (uint32_t)(w >> 32));
 }
 
 // DPP helpers (gfx9 row_shr / row_bcast; identity 0 for lanes without a source)
@@ -270,15 +269,15 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("" ::: "memory");
 }
 
-// Encode the staged block (n bytes at S.buf[kInOff]) into S.buf[kOutOff ...];
-// returns the bytes written.  kMatchesOnly: stop after the best-match scan
-// and store every position's find_longest_match result to mout instead
-// (lz4r_block_matches_device).
+// Encode the staged block (n bytes at S.buf[kInOff]) as sequence records at
+// recs (global: the block's slot); returns the bytes its stream takes.
+// kMatchesOnly: stop after the best-match scan and store every position's
+// find_longest_match result to mout instead (lz4r_block_matches_device).
 template <bool kMatchesOnly>
-__device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restrict__ mout) {
+__device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restrict__ mout,
+                                            uint32_t *__restrict__ recs) {
   const int lane = threadIdx.x;
   constexpr int base = kInOff;
-  constexpr int obase = kOutOff;
 
   // ---- index: per-bucket chains of the 4-gram starts -----------------------
   // Position p swaps itself (+1) into its bucket's head and keeps the
@@ -547,13 +546,15 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     wave_sync();
   }
   PROF_MARK(5);                       // walk
-  // ---- sequences: lane kk = sequence kk ------------------------------------
+  // ---- sequence records: lane kk = sequence kk -----------------------------
   // A round is 64 consecutive sequences; the match sequences are a prefix
   // (cpos < n), followed by the literal-only tail when the last match ends
   // before n (LZ4.c:585-612).  Rounds go on while a round is all matches.
-  if (lane < kBlkOutMax / 16)          // the output area starts zeroed: bytes land by ds_or
-    reinterpret_cast<uint4 *>(S.buf + obase)[lane] = make_uint4(0, 0, 0, 0);
-  wave_sync();
+  // The block leaves as records -- sequence k: its match start | M << 9 |
+  // dist << 17 (its literal run starts where sequence k - 1's match ends; the
+  // tail is n | 0 | 0) -- after a header dword, the sum of the sequences'
+  // size fields | the sequence count << 16.  lz4_emit writes the bytes
+  // (write_sequence / write_block, LZ4.c:365-425) straight into the stream.
   int nseq = 0;
   int ocar = 3;                      // block header: u8 nseq, u16 size
   int szsum = 0;
@@ -591,76 +592,15 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     const uint32_t ws = act ? (uint32_t)(5 + le + L) * 0x10001u + (mextW ? 1u : 0u) +
                                   (mextS ? 0x10000u : 0u)
                             : 0u;
-    const uint32_t inc = wave_incl_add(ws);
-    const uint32_t tot = lane63(inc);
-    const int excl = (int)((inc - ws) & 0xFFFFu);
-    // Every LDS access of the emission is naturally aligned (a misaligned
-    // ds_read/ds_write is replayed by the LDS at ~1-2 cycles per lane): the
-    // output area is zeroed and every byte lands by an aligned ds_or.
-    const int o = obase + ocar + excl;
-    const int ol = o + 3 + le;                                         // first literal byte
-    uint32_t *const out32 = reinterpret_cast<uint32_t *>(S.buf);
-    if (act) {
-      const int tl = L >= 15 ? 15 : L;                                // LZ4.c:540
-      const int tm = M == 0 ? 0 : (M >= 19 ? 15 : mx);                // LZ4.c:542
-      // token, u16 size, literal-extension bytes (LZ4.c:367-386): [rem] or [255, 0]
-      const uint32_t ext = le == 0 ? 0u : (rem == 255 ? 255u : (uint32_t)rem);
-      const uint32_t SZ = (ws >> 16) & 0xFFFFu;
-      or_bytes(out32, o, (uint32_t)((tl << 4) | tm) | (SZ << 8) | (ext << 24));
-      // offset (LZ4.c:390) and match extension (LZ4.c:393-411)
-      or_bytes(out32, ol + L, (uint32_t)D | (mextW ? ((uint32_t)(mx - 15) & 255u) << 16 : 0u));
-    }
-    // literals (LZ4.c:388), flattened over the lanes: one aligned 8-byte
-    // output word per lane and round, its bytes funnel-shifted out of two
-    // aligned input words and masked to the run
-    {
-      const int cw = act && L > 0 ? ((ol + L - 1) >> 3) - (ol >> 3) + 1 : 0;   // words of the run
-      const uint32_t cinc = wave_incl_add((uint32_t)cw);
-      // exclusive prefix by a lane shift (cinc - cw made the compiler keep
-      // every partial of the scan to re-add them)
-      const int C = (int)lane63(cinc), st = (int)dpp<0x138, 0xf, 0xf>(cinc);
-      const uint32_t prm = (uint32_t)ol | ((uint32_t)L << 10) | ((uint32_t)pend << 19);
-      uint32_t carry = 0;                        // 1 + the last run owning a word so far
-      for (int g0 = 0; g0 < C; g0 += 64) {
-        wave_sync();
-        S.cand()[lane] = 0u;                       // run-start marks of this round
-        if (cw > 0 && st >= g0 && st < g0 + 64) S.cand()[st - g0] = (uint32_t)lane + 1u;
-        wave_sync();                             // marks of other lanes: no forwarding
-        const uint32_t k1 = max(wave_incl_max(S.cand()[lane]), carry);
-        carry = lane63(k1);
-        const int g = g0 + lane;
-        const int k = (int)k1 - 1;               // the run owning word g
-        const uint32_t pk = (uint32_t)__shfl((int)prm, k & 63, 64);
-        const int sk = __shfl(st, k & 63, 64);
-        if (g < C) {
-          const int kol = (int)(pk & 1023u), kL = (int)((pk >> 10) & 511u);
-          const int kpend = (int)(pk >> 19);
-          const int w = (kol >> 3) + (g - sk);                         // output word
-          const int xs = 8 * w + base + kpend - kol;                   // its input bytes
-          const uint64_t *iw = reinterpret_cast<const uint64_t *>(S.buf + (xs & ~7));
-          const uint64_t lo = iw[0], hi = iw[1];
-          const uint32_t sh = 8u * (uint32_t)(xs & 7);
-          const uint64_t v = (lo >> sh) | ((hi << 1) << (63u - sh));
-          const int lb = max(kol - 8 * w, 0), hb = min(kol + kL - 8 * w, 8);
-          const uint64_t mask = (~0ull << (8 * lb)) & (~0ull >> (64 - 8 * hb));
-          atomicOr(reinterpret_cast<unsigned long long *>(S.buf + 8 * w),
-                   (unsigned long long)(v & mask));
-        }
-      }
-    }
+    const uint32_t tot = lane63(wave_incl_add(ws));
+    if (act) recs[1 + kk] = (uint32_t)cpos | ((uint32_t)M << 9) | ((uint32_t)D << 17);
     ocar += (int)(tot & 0xFFFFu);
     szsum += (int)(tot >> 16);
     nseq += (int)__popcll(ballot(act));
     if (nm_r < 64) break;
   }
-  PROF_MARK(6);                       // emission
-  if (lane == 0) {                                                     // LZ4.c:417-419
-    const int bsz = szsum + 3;
-    S.buf[obase] = (uint8_t)nseq;
-    S.buf[obase + 1] = (uint8_t)(bsz & 255);
-    S.buf[obase + 2] = (uint8_t)((bsz >> 8) & 255);
-  }
-  wave_sync();
+  PROF_MARK(6);                       // records
+  if (lane == 0) recs[0] = (uint32_t)szsum | ((uint32_t)nseq << 16);
   return ocar;
 }
 
@@ -694,10 +634,8 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   }
   wave_sync();
 
-  const int W = encode_block<false>(S, n, nullptr);
-  // the block's bytes -> its 16-B aligned slot (<= 35 chunks: one round)
-  uint4 *dst = reinterpret_cast<uint4 *>(slots + (size_t)t * kSlot);
-  if (lane < ((W + 15) >> 4)) dst[lane] = reinterpret_cast<const uint4 *>(S.buf + kOutOff)[lane];
+  const int W = encode_block<false>(S, n, nullptr,
+                                   reinterpret_cast<uint32_t *>(slots + (size_t)t * kSlot));
   if (lane == 0) {
     usz[t] = (uint32_t)W;
     bsizes[t] = (uint16_t)W;
@@ -717,7 +655,7 @@ __global__ __launch_bounds__(64) void lz4_matches(const uint8_t *__restrict__ in
   for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
   if (lane < 16) S.buf[kInOff + n + lane] = 0;
   wave_sync();
-  encode_block<true>(S, n, mout + (size_t)t * kBlk);
+  encode_block<true>(S, n, mout + (size_t)t * kBlk, nullptr);
 }
 
 // ---- placement: exclusive scan of tile sizes, then gather -----------------
@@ -784,25 +722,51 @@ __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__
 
 
 
-// Workgroup = group of 64 consecutive blocks.  Offsets from the partials, the
-// group sums and a wave scan.  The group's bytes are assembled in LDS: each
-// slot's 16-B chunks are read with aligned, coalesced loads (the four waves
-// take 16 slots each, chunks flattened over the lanes) and written at the
-// slot's place in the output range (unaligned LDS stores; a slot's last chunk
-// writes its W % 16 bytes exactly, so slots never overwrite each other).
-// Then the range leaves as aligned 16-B stores; only the group's two edge
-// chunks are written bytewise.  Also writes the frame byte (LZ4.c:429).
-constexpr int kGH = 32;                              // blocks per gather workgroup
+// lz4_emit: workgroup = 32 consecutive blocks (half a scan group of 64).
+//   offsets  the blocks' stream offsets from the partials, the group sums and
+//            a wave scan; also stored to boff (the decoder's side input)
+//   stage    the 32 blocks' input -> LDS (the literals' source; 16-B loads)
+//   bytes    each wave takes 8 blocks and flattens their sequence records over
+//            the lanes (one round = 64 sequences of one or more blocks); per
+//            sequence the token / size / literal-extension / offset /
+//            match-extension bytes (write_sequence, LZ4.c:365-413) and per
+//            block the u8 count + u16 size header (write_block, :415-425)
+//            land by aligned ds_or in a zeroed LDS image of the output range,
+//            and the literal runs are flattened over the lanes as aligned
+//            8-byte image words funnel-shifted out of the staged input
+//   store    the image -> the stream as aligned 16-B stores (the edge chunks
+//            bytewise); nothing at or past `cap` is written.
+// This is the emission lz4_tiles used to do one block per wave; here a round
+// serves several blocks and the kernel is bound by its HBM traffic, not by
+// instruction issue as lz4_tiles is.
+constexpr int kGH = 32;                              // blocks per emit workgroup
+constexpr int kEW = 8;                               // waves per emit workgroup (4 blocks each)
+constexpr int kRecPre = 32;                          // record dwords per block staged in LDS
 constexpr int kGSplit = kGT / kGH;                   // workgroups per group
-constexpr int kGatherLds = kGH * kBlkOutMax + 32;    // worst case: every block 548 B
-__global__ __launch_bounds__(256) void lz4_gather(
-    const uint8_t *__restrict__ slots, size_t slot_base, const uint32_t *__restrict__ tsz,
-    size_t ntiles, size_t g_first, const uint32_t *__restrict__ gsum,
-    const uint64_t *__restrict__ part, uint8_t *__restrict__ out, uint64_t cap, int hdr,
-    uint64_t nb_total, uint64_t *__restrict__ boff) {
+constexpr int kEmitImg = kGH * kBlkOutMax + 32;      // worst case: every block 548 B
+constexpr int kStagePad = 16;                        // literal words reach 8 B before a run
+constexpr int kStage = kStagePad + kGH * kBlk + 32;  // ... and 16 B past its end
+static_assert(kStage < (1 << 16), "stage offsets fit 16 bits");
+
+// OR the (<= 4) bytes of v into the zeroed byte area at offset x: two
+// aligned dwords (ds_or_b32), never a misaligned access
+__device__ __forceinline__ void or_bytes(uint32_t *buf32, int x, uint32_t v) {
+  const uint64_t w = (uint64_t)v << (8 * (x & 3));
+  atomicOr(&buf32[x >> 2], (uint32_t)w);
+  atomicOr(&buf32[(x >> 2) + 1], (uint32_t)(w >> 32));
+}
+
+__global__ __launch_bounds__(64 * kEW) void lz4_emit(
+    const uint8_t *__restrict__ in, const uint8_t *__restrict__ slots, size_t slot_base,
+    const uint32_t *__restrict__ tsz, size_t ntiles, size_t g_first,
+    const uint32_t *__restrict__ gsum, const uint64_t *__restrict__ part,
+    uint8_t *__restrict__ out, uint64_t cap, int hdr, uint64_t nb_total, uint32_t last_n,
+    uint64_t *__restrict__ boff) {
   __shared__ uint64_t toff[kGT + 1];
-  __shared__ uint32_t cex[kGT + 1];                  // exclusive chunk counts
-  __shared__ alignas(16) uint8_t img[kGatherLds];
+  __shared__ alignas(16) uint8_t img[kEmitImg];
+  __shared__ alignas(16) uint8_t stage[kStage];
+  __shared__ uint32_t marks[kEW][64];                // per wave: literal-run starts
+  __shared__ uint32_t recst[kGH][kRecPre];           // each block's header + first records
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const size_t g = g_first + blockIdx.x / kGSplit;
   const int h0 = (int)(blockIdx.x % kGSplit) * kGH;  // this workgroup: blocks [h0, h0 + kGH)
@@ -823,48 +787,148 @@ __global__ __launch_bounds__(256) void lz4_gather(
     // device-resident block offsets (relative to the first block byte) for
     // the block-parallel decoder: no host prefix sum, no host round trip
     if (h0 == 0 && tid < nt) boff[g0 + tid] = base + inc - v - (uint64_t)hdr;
-    const uint32_t ck = (tid >= h0 && tid < h1) ? (v + 15u) >> 4 : 0u;
-    const uint32_t cinc = wave_incl_add(ck);
-    cex[tid] = cinc - ck;
-    if (tid == 63) cex[kGT] = cinc;
   }
   __syncthreads();
   if (hdr && g == 0 && h0 == 0 && tid == 0 && cap > 0) out[0] = (uint8_t)nb_total;
   const uint64_t G0 = toff[h0];
   const uintptr_t abs0 = (uintptr_t)(out + G0);
   const int lead = (int)(abs0 & 15);               // img[lead] = stream byte G0
-  // zero the image: every byte then lands by an aligned ds_or (a misaligned
-  // LDS store is replayed at ~2 cycles per lane)
   {
     const int span = lead + (int)(toff[h1] - G0);
-    for (int i = tid; i < (span + 15) >> 4; i += 256)
+    for (int i = tid; i < (span + 15) >> 4; i += 64 * kEW)
       reinterpret_cast<uint4 *>(img)[i] = make_uint4(0, 0, 0, 0);
   }
-  __syncthreads();
-  // ---- slots -> LDS image -----------------------------------------------------
+  // the blocks' record heads (one 16-B load per thread: 32 slots x 128 B)
   {
-    constexpr int kPer = kGH / 4;                  // slots per wave
-    const int s0 = h0 + wv * kPer, s1 = min(h1, s0 + kPer);
-    if (s0 < s1) {
-      const int c0 = (int)cex[s0], c1 = (int)cex[s1];
-      int t = s0;                                  // slot cursor (chunks ascend per lane)
-      for (int c = c0 + lane; c < c1; c += 64) {
-        while (t + 1 < s1 && (int)cex[t + 1] <= c) ++t;
-        const int j = c - (int)cex[t];
-        const uint4 v =
-            reinterpret_cast<const uint4 *>(slots + (g0 + t - slot_base) * (size_t)kSlot)[j];
-        const int x = lead + (int)(toff[t] - G0) + 16 * j;      // image byte of the chunk
-        const int m = (int)(toff[t + 1] - toff[t]) - 16 * j;   // bytes of this slot left
-        uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
-        uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
-        lo &= m >= 8 ? ~0ull : (1ull << (8 * m)) - 1ull;          // m >= 1
-        hi &= m >= 16 ? ~0ull : (m <= 8 ? 0ull : (1ull << (8 * (m - 8))) - 1ull);
-        // the 16 bytes shifted by x & 7 over three aligned 8-byte words
-        const uint32_t sh = 8u * (uint32_t)(x & 7);
-        unsigned long long *w = reinterpret_cast<unsigned long long *>(img + (x & ~7));
-        atomicOr(&w[0], (unsigned long long)(lo << sh));
-        atomicOr(&w[1], (unsigned long long)((hi << sh) | ((lo >> 1) >> (63u - sh))));
-        atomicOr(&w[2], (unsigned long long)((hi >> 1) >> (63u - sh)));
+    constexpr int kPerSlot = kRecPre / 4;
+    for (int i = tid; i < (h1 - h0) * kPerSlot; i += 64 * kEW) {
+      const int hb = i / kPerSlot, j = i % kPerSlot;
+      reinterpret_cast<uint4 *>(&recst[hb][0])[j] = reinterpret_cast<const uint4 *>(
+          slots + (g0 + h0 + hb - slot_base) * (size_t)kSlot)[j];
+    }
+  }
+  // ---- stage: byte p of block h is stage[kStagePad + 300 (h - h0) + p] ----------
+  {
+    const size_t b0 = g0 + h0;
+    const uint8_t *src = in + b0 * kBlk;
+    const int len = (h1 - h0 - 1) * kBlk + (g0 + h1 == nb_total ? (int)last_n : kBlk);
+    uint8_t *dst = stage + kStagePad;
+    if (((uintptr_t)src & 15) == 0) {              // b0 is a multiple of 32: 9600 B steps
+      const int n16 = len >> 4;
+      for (int i = tid; i < n16; i += 64 * kEW)
+        reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+      for (int i = (n16 << 4) + tid; i < len; i += 64 * kEW) dst[i] = src[i];
+    } else {
+      for (int i = tid; i < len; i += 64 * kEW) dst[i] = src[i];
+    }
+  }
+  __syncthreads();
+  // ---- records -> bytes: wave wv takes blocks [bl0, bl1) ------------------------
+  {
+    constexpr int kBW = kGH / kEW;                   // blocks per wave
+    const int bl0 = h0 + wv * kBW, bl1 = min(h1, bl0 + kBW);
+    if (bl0 < bl1) {
+      uint32_t *const out32 = reinterpret_cast<uint32_t *>(img);
+      const int nbk = bl1 - bl0;
+      // lanes 0..nbk-1: the blocks' sequence counts -> first flattened index
+      const uint32_t hd = lane < nbk ? recst[bl0 - h0 + lane][0] : 0u;
+      const uint32_t ns = hd >> 16;
+      const uint32_t sinc = wave_incl_add(ns);
+      const int Stot = (int)lane63(sinc);
+      const int sst = (int)(sinc - ns);
+      int st[kBW];                                 // wave-uniform block starts
+#pragma unroll
+      for (int i = 0; i < kBW; ++i)
+        st[i] = i < nbk ? __builtin_amdgcn_readlane(sst, i) : 0x7fffffff;
+      int end_prev = 0, cont = 0;
+      for (int f0 = 0; f0 < Stot; f0 += 64) {
+        const int f = f0 + lane;
+        const bool valid = f < Stot;
+        int bi = 0, sb = 0;                        // the lane's block: the last start <= f
+#pragma unroll
+        for (int i = 1; i < kBW; ++i) {
+          const bool ge = f >= st[i];
+          bi += ge ? 1 : 0;
+          sb = ge ? st[i] : sb;
+        }
+        const int k = f - sb;                      // sequence index in the block
+        const int hb = bl0 + bi;
+        const size_t tb = g0 + hb;                 // block index of the call
+        const uint32_t *rp =
+            reinterpret_cast<const uint32_t *>(slots + (tb - slot_base) * (size_t)kSlot);
+        const uint32_t r = !valid ? 0u : (1 + k < kRecPre ? recst[hb - h0][1 + k] : rp[1 + k]);
+        const int cpos = (int)(r & 511u);
+        const int M = (int)((r >> 9) & 255u), D = (int)(r >> 17);
+        const int end = cpos + M;
+        const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
+        const int pend = k == 0 ? 0 : (lane == 0 ? end_prev : (int)upv);   // literal run start
+        end_prev = (int)lane63((uint32_t)end);
+        const int L = cpos - pend;
+        const int rem = (L - 15) & 255;
+        const int le = L >= 15 ? (rem == 255 ? 2 : 1) : 0;         // literal-extension bytes
+        const int mx = (M - 4) & 255;
+        const bool mextW = M >= 4 && mx >= 15, mextS = M != 0 && mx >= 15;
+        const int bytes = valid ? 5 + le + L + (mextW ? 1 : 0) : 0;
+        const uint32_t inc = wave_incl_add((uint32_t)bytes);
+        // offsets restart at every block; the round's first block may continue
+        // one that began in an earlier round (it then starts at `cont`)
+        // (the cross-lane read stays outside any select: in a divergent region
+        // ds_bpermute would read 0 from the lanes the select turned off)
+        const int incb = __shfl((int)inc, max(sb - f0 - 1, 0), 64);
+        const int segb = sb > f0 ? incb : 0;
+        const int orel = 3 + (int)inc - bytes - segb + (sb < f0 ? cont : 0);
+        const int ib = lead + (int)(toff[hb] - G0);                  // block's first image byte
+        const int o = ib + orel;
+        const int ol = o + 3 + le;                                   // first literal byte
+        if (valid) {
+          const int tl = L >= 15 ? 15 : L;                            // LZ4.c:540
+          const int tm = M == 0 ? 0 : (M >= 19 ? 15 : mx);            // LZ4.c:542
+          const uint32_t ext = le == 0 ? 0u : (rem == 255 ? 255u : (uint32_t)rem);
+          const uint32_t SZ = (uint32_t)(5 + le + L + (mextS ? 1 : 0));   // LZ4.c:546-575
+          or_bytes(out32, o, (uint32_t)((tl << 4) | tm) | (SZ << 8) | (ext << 24));
+          or_bytes(out32, ol + L, (uint32_t)D | (mextW ? ((uint32_t)(mx - 15) & 255u) << 16 : 0u));
+          if (k == 0) {                                               // LZ4.c:417-419
+            const uint32_t bh = recst[hb - h0][0];
+            or_bytes(out32, ib, ((bh >> 16) & 255u) | ((((bh & 0xFFFFu) + 3u) & 0xFFFFu) << 8));
+          }
+        }
+        // literals (LZ4.c:388), flattened over the lanes: one aligned 8-byte
+        // image word per lane and pass, funnel-shifted out of two aligned
+        // staged input words and masked to the run
+        {
+          const int cw = valid && L > 0 ? ((ol + L - 1) >> 3) - (ol >> 3) + 1 : 0;
+          const uint32_t cinc = wave_incl_add((uint32_t)cw);
+          const int C = (int)lane63(cinc), stw = (int)dpp<0x138, 0xf, 0xf>(cinc);
+          const int lsrc = (L << 16) | (kStagePad + kBlk * (hb - h0) + pend);
+          uint32_t carry = 0;                    // 1 + the last run owning a word so far
+          for (int w0 = 0; w0 < C; w0 += 64) {
+            wave_sync();
+            marks[wv][lane] = 0u;
+            if (cw > 0 && stw >= w0 && stw < w0 + 64) marks[wv][stw - w0] = (uint32_t)lane + 1u;
+            wave_sync();
+            const uint32_t k1 = max(wave_incl_max(marks[wv][lane]), carry);
+            carry = lane63(k1);
+            const int gw = w0 + lane;
+            const int kr = ((int)k1 - 1) & 63;   // the run owning word gw
+            const int kol = __shfl(ol, kr, 64);
+            const int kls = __shfl(lsrc, kr, 64);
+            const int sk = __shfl(stw, kr, 64);
+            if (gw < C) {
+              const int kL = kls >> 16, ksrc = kls & 0xFFFF;
+              const int w = (kol >> 3) + (gw - sk);                   // image word
+              const int xs = 8 * w + ksrc - kol;                       // its input bytes
+              const uint64_t *iw = reinterpret_cast<const uint64_t *>(stage + (xs & ~7));
+              const uint64_t lo = iw[0], hi = iw[1];
+              const uint32_t sh = 8u * (uint32_t)(xs & 7);
+              const uint64_t v = (lo >> sh) | ((hi << 1) << (63u - sh));
+              const int lb = max(kol - 8 * w, 0), hbb = min(kol + kL - 8 * w, 8);
+              const uint64_t mask = (~0ull << (8 * lb)) & (~0ull >> (64 - 8 * hbb));
+              atomicOr(reinterpret_cast<unsigned long long *>(img + 8 * w),
+                       (unsigned long long)(v & mask));
+            }
+          }
+        }
+        cont = (int)lane63((uint32_t)(orel + bytes - 3));  // bytes of lane 63's block so far
       }
     }
   }
@@ -875,7 +939,7 @@ __global__ __launch_bounds__(256) void lz4_gather(
   const uintptr_t absend = (uintptr_t)(out + G1);
   const uintptr_t first = abs0 & ~(uintptr_t)15;
   const int nchunks = (int)((absend - first + 15) >> 4);
-  for (int ci = tid; ci < nchunks; ci += 256) {
+  for (int ci = tid; ci < nchunks; ci += 64 * kEW) {
     const uintptr_t a = first + ((uintptr_t)ci << 4);
     const uint4 v = reinterpret_cast<const uint4 *>(img)[ci];
     if (a >= abs0 && a + 16 <= absend) {
@@ -915,7 +979,7 @@ struct lz4r_ctx {
   size_t cap_slots = 0;        // capacity of the slot scratch, in blocks (<= kChunk)
   uint16_t *bsizes = nullptr;  // encoded bytes of every block of the last call
   uint64_t *boff = nullptr;    // every block's offset from the first block byte
-  uint8_t *slots = nullptr;    // per-block output slots (kSlot bytes each), one chunk
+  uint8_t *slots = nullptr;    // per-block record slots (kSlot bytes each), one chunk
   uint32_t *tsz = nullptr;     // encoded bytes per block (u32, for the scan)
   uint32_t *gsum = nullptr;    // encoded bytes per group of kGT blocks
   uint64_t *part = nullptr;    // scan partials, one per kPart blocks
@@ -1019,9 +1083,10 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
     hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part + p0, np,
                        (uint64_t)hdr, k == 0 ? 1 : 0, static_cast<uint64_t *>(d_len));
     const size_t g0 = b0 / kGT, ng = (nbc + kGT - 1) / kGT;
-    hipLaunchKernelGGL(lz4_gather, dim3((unsigned)(ng * kGSplit)), dim3(256), 0, s, c->slots,
+    hipLaunchKernelGGL(lz4_emit, dim3((unsigned)(ng * kGSplit)), dim3(64 * kEW), 0, s, in, c->slots,
                        b0, c->tsz, b1, g0, c->gsum, c->part, static_cast<uint8_t *>(d_out),
-                       (uint64_t)cap, hdr, (uint64_t)nb, c->boff);
+                       (uint64_t)cap, hdr, (uint64_t)nb, (uint32_t)(n - (nb - 1) * kBlk),
+                       c->boff);
   }
   if (timed) (void)hipEventRecord(c->ev_c, s);
   c->last_nb = nb;
