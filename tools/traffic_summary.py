@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic of lz4_tiles and jpeg_strip_kernel from the PMC
+"""Per-launch HBM traffic of lz4_tiles, lz4_emit, jpeg_strip_kernel and the others from the PMC
 passes written by tools/traffic.sh.
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB (summed over
@@ -25,7 +25,7 @@ def per_launch(db, counter, kernel_sub):
 
 def main(d):
     out = {}
-    for kern, run, sub in (("lz4", "lz4", "lz4_tiles"), ("lz4_gather", "lz4", "lz4_gather"),
+    for kern, run, sub in (("lz4", "lz4", "lz4_tiles"), ("lz4_emit", "lz4", "lz4_emit"),
                            ("jpeg", "jpeg", "jpeg_strip_kernel"),
                            ("lz4_decode", "dec", "lz4_decode_blocks"),
                            ("entropy_encode", "ent", "entropy_encode_fast"),
