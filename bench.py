@@ -362,6 +362,30 @@ def run_lz4(ctx, n_total, scaling):
     }
     log(f"lz4 decode: {dec_kern_ms:.3f} ms/launch, {lz4_dec['value']} GB/s, ok={dec_ok}")
 
+    # the same stream decoded from the bytes alone (LZ4_decode, LZ4.c:1038):
+    # block boundaries found on the device, then the block decoder
+    d_dec = torch.empty(n + 300, dtype=torch.uint8, device=dev)
+    _, got = lz4.decompress_stream_device(d_out, flen, n + 300, d_out=d_dec)
+    bare_ok = got == n and bool(torch.equal(d_dec[:n], d_in[:n]))
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lz4.decompress_stream_device(d_out, flen, n + 300, d_out=d_dec)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    bdt = ctx.max_over_ranks(time.perf_counter() - t0)
+    bare_ok = ctx.sum_over_ranks(0 if bare_ok else 1) == 0
+    del d_dec
+    lz4_dec["bare_stream"] = {
+        "metric": "LZ4 decode GB/s from the stream alone (lz4r_decompress_stream_device)",
+        "value": round(n_total / (bdt / args.steps) / 1e9, 3), "unit": "GB/s",
+        "call_ms": round(bdt / args.steps * 1e3, 4), "roundtrip_ok": bare_ok,
+        "note": "whole synchronous call: on-device block-boundary discovery (lz4_bare_*), "
+                "lz4_decode_blocks, two host read-backs"}
+    log(f"lz4 bare-stream decode: {bdt / args.steps * 1e3:.3f} ms/call, "
+        f"{lz4_dec['bare_stream']['value']} GB/s, ok={bare_ok}")
+
     # N > 1: assemble the framed stream on rank 0 (RCCL gatherv over xGMI)
     gather_ms = gather_ok = None
     if world > 1:

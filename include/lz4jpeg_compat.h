@@ -14,9 +14,10 @@
  *                                 LZ4Frame (LZ4.c:30-52)
  *   write_output               <- LZ4.c:365-441
  *   LZ4_decode                 <- LZ4.c:1038-1121
- *       decodes input_bin_file into LZ4_UNCOMPRESSED_FILE with the exact
- *       decoder (lz4r_decompress); `log` is opened for append like the
- *       reference and left untouched.
+ *       decodes input_bin_file into LZ4_UNCOMPRESSED_FILE on the GPU from
+ *       the stream alone (lz4r_decompress_stream: block boundaries found on
+ *       the device); `log` is opened for append like the reference and left
+ *       untouched.
  *   discrete_cosine_transform  <- Algorithms/sequential/JPEG/JPEG.c:451-494
  *       width 8 or 4, height 8 (the shapes the reference calls); mallocs
  *       *coefficients (caller frees, JPEG.c:1447).  GPU: jpegr_dct_blocks_device.

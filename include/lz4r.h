@@ -145,6 +145,24 @@ int lz4r_decompress_device(const void *d_in, size_t in_len, const void *d_block_
                            size_t nb, void *d_out, size_t out_cap, void *d_result,
                            void *stream);
 
+/* Decode a bare framed stream on the GPU -- only the stream, as LZ4_decode
+ * (LZ4.c:1038) takes the file: the block boundaries are found on the device
+ * (csrc/lz4r_gpudec.hip: a candidate header per 4 KiB chunk, a lane per
+ * chunk walking the size fields, one wave re-walking any chunk whose
+ * predecessor does not end on its candidate), then lz4_decode_blocks checks
+ * every block against them.  Streams with truncated matches (whose size
+ * fields over-count, LZ4.c:569-575) take a second pass that parses every
+ * block.  d_in / d_out are device pointers; synchronises `stream`;
+ * *out_len = decoded length.  LZ4R_ERR_CORRUPT when the blocks do not chain
+ * from the frame byte to the end of the stream or a block does not decode;
+ * LZ4R_ERR_CAPACITY (with *out_len = need) when out_cap is too small. */
+int lz4r_decompress_stream_device(const void *d_in, size_t in_len, void *d_out,
+                                  size_t out_cap, size_t *out_len, void *stream);
+
+/* Host-buffer form of lz4r_decompress_stream_device (copies in and out). */
+int lz4r_decompress_stream(const uint8_t *in, size_t in_len, uint8_t *out, size_t cap,
+                           size_t *out_len);
+
 /* Host convenience wrapper around lz4r_compress_device (copies in and out). */
 int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
                   size_t *out_len);

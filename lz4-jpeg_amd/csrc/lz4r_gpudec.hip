@@ -241,7 +241,12 @@ __device__ __forceinline__ void copy_match(const SlotT &o, int q, int D, int M) 
 // soon as the next ip is known (it does not depend on the distance: the
 // literal-only tail has tm = 0, so no match-extension byte either way), so
 // its load overlaps this sequence's copies.
-template <typename BytesT, typename SlotT>
+// kFindLen: the block's end is unknown (a bare stream, lz4_bare_walk's exact
+// mode): `len` is the bytes readable from the block start (<= kInMax), the
+// block ends at the first complete reading (300 bytes, or 1..300 ending at
+// `len` when `last`), and the return value is its byte length, not the
+// decoded length (0 = no reading).
+template <typename BytesT, typename SlotT, bool kFindLen = false>
 __device__ __forceinline__ int decode_block(const BytesT &p, int len, bool last, const SlotT &o) {
   uint32_t stk[kDepth];                              // choice points (registers; rare)
   const uint64_t h0 = p.ld8(0);
@@ -256,7 +261,11 @@ __device__ __forceinline__ int decode_block(const BytesT &p, int len, bool last,
     V16 hn = {0, 0};
     if (++steps > kMaxSteps) return 0;
     if (k == nseq) {
-      if (ip == len && ip - 3 + ntr == want && (pos == kBlk || (last && pos >= 1))) return pos;
+      if constexpr (kFindLen) {
+        if (ip - 3 + ntr == want && (pos == kBlk || (last && ip == len && pos >= 1))) return ip;
+      } else {
+        if (ip == len && ip - 3 + ntr == want && (pos == kBlk || (last && pos >= 1))) return pos;
+      }
     } else if (ip + 3 <= len) {
       const int tok = (int)(h.lo & 255), Sz = (int)((h.lo >> 8) & 0xFFFF);
       const int e0 = (int)((h.lo >> 24) & 255), e1 = (int)((h.lo >> 32) & 255);
@@ -392,6 +401,254 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
   }
 }
 
+// ---- bare streams: block boundaries found on the device ---------------------
+// LZ4_decode (LZ4.c:1038) takes only the file.  The stream is cut into
+// chunks of kChunkB bytes; in each chunk the first position that parses as
+// a block header is a candidate start (lz4_bare_cand), a lane per chunk
+// walks the blocks from its candidate to the next chunk (lz4_bare_walk),
+// and one wave checks that every chunk's walk ends on the next chunk's
+// candidate, re-walking a chunk from its predecessor's exit where it does
+// not (lz4_bare_fix).  By induction from position 1 the candidates are then
+// on the stream's own block chain.  A block's length is its u16 size field
+// (fast mode) unless it holds truncated matches (M = 1..3, LZ4.c:317), whose
+// size fields count a byte that is never written (LZ4.c:569-575): the exact
+// mode parses every block (decode_block<kFindLen>).  The host tries the
+// fast mode first; the decoder checks every block against its boundaries,
+// so a wrong fast-mode boundary is an error, never wrong bytes.
+constexpr int kChunkB = 4096;                        // stream bytes per chunk
+constexpr int kWin = 2 * kInMax + 32;                // candidate window (LDS)
+constexpr uint64_t kNone = ~0ull;                    // no candidate in the chunk
+constexpr uint64_t kBad = ~0ull - 1;                 // the walk met an impossible block
+
+// a slot that stores nothing and reads zeros: decode_block as a parser
+struct NullSlot {
+  __device__ __forceinline__ uint64_t ld8(int) const { return 0; }
+  __device__ __forceinline__ V16 ld16(int) const { return {0, 0}; }
+  __device__ __forceinline__ void st_fast(int, V16, int) const {}
+  __device__ __forceinline__ void st(int, V16, int) const {}
+};
+
+__device__ __forceinline__ int rd_u16(const uint8_t *w, int a) {
+  return (int)w[a] | ((int)w[a + 1] << 8);
+}
+
+// Candidate start of every chunk: a wave per chunk, its window
+// [s, s + kWin) of the stream in LDS.  x passes when its header is
+// plausible (1 <= nseq, 3 + 5 nseq <= size <= kInMax, inside the stream) and
+// the nseq sequence size fields, hopped as written, end exactly at x + size
+// (a true block without truncated matches always does), and the next header
+// is plausible too (or x + size is the stream end).
+__global__ __launch_bounds__(256) void lz4_bare_cand(const uint8_t *__restrict__ in,
+                                                      size_t in_len, size_t nchunks,
+                                                      uint64_t *__restrict__ cand) {
+  __shared__ alignas(16) uint8_t win[4][kWin + 16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const size_t c = (size_t)blockIdx.x * 4 + wv;
+  if (c >= nchunks) return;
+  if (c == 0) {                                      // the first block starts after the frame byte
+    if (lane == 0) cand[0] = 1;
+    return;
+  }
+  const size_t s = 1 + c * (size_t)kChunkB;
+  uint8_t *w = win[wv];
+  for (int i = lane; i < kWin; i += 64) w[i] = s + i < in_len ? in[s + i] : 0;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const int avail = (int)min((size_t)kWin, in_len - s);   // window bytes inside the stream
+  uint64_t found = kNone;
+  for (int x0 = 0; x0 < kInMax && x0 < avail; x0 += 64) {
+    const int x = x0 + lane;
+    bool ok = x + 3 <= avail;
+    int nseq = 0, size = 0;
+    if (ok) {
+      nseq = w[x];
+      size = rd_u16(w, x + 1);
+      ok = nseq >= 1 && size >= 3 + 5 * nseq && size <= kInMax && x + size <= avail;
+    }
+    if (ok) {
+      int y = x + 3;
+      for (int k = 0; k < nseq && ok; ++k) {
+        const int S = y + 3 <= x + size ? rd_u16(w, y + 1) : 0;
+        ok = S >= 5;
+        y += S;
+        ok = ok && y <= x + size;
+      }
+      ok = ok && y == x + size;
+      if (ok && s + (size_t)(x + size) < in_len) {   // the next header
+        const int z = x + size;
+        ok = z + 3 <= avail && w[z] >= 1 && rd_u16(w, z + 1) >= 8 && rd_u16(w, z + 1) <= kInMax;
+      }
+    }
+    const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+    if (m) {
+      found = s + (size_t)(x0 + __builtin_ctzll(m));
+      break;
+    }
+  }
+  if (lane == 0) cand[c] = found;
+}
+
+// the byte length of the block at x (0: no block can start there)
+template <bool kExact>
+__device__ __forceinline__ int bare_block_len(const uint8_t *in, size_t in_len, size_t x) {
+  if (x + 3 > in_len) return 0;
+  const int size = (int)in[x + 1] | ((int)in[x + 2] << 8);
+  if (!kExact) return in[x] >= 1 && size >= 8 && size <= kInMax && x + size <= in_len ? size : 0;
+  const size_t rem = in_len - x;
+  const int len = rem < (size_t)kInMax ? (int)rem : kInMax;
+  return decode_block<Bytes<true>, NullSlot, true>(Bytes<true>{in + x, rem}, len,
+                                                   rem <= (size_t)kInMax, NullSlot{});
+}
+
+// the blocks of chunk c from x: count and exit (the first position at or
+// past the next chunk), or kBad; kWrite: their offsets to boff[base ...]
+template <bool kExact, bool kWrite>
+__device__ __forceinline__ uint64_t bare_walk_chunk(const uint8_t *in, size_t in_len, size_t c,
+                                                    uint64_t x, uint32_t &cnt,
+                                                    uint64_t *boff, uint64_t base) {
+  cnt = 0;
+  if (x == kNone || x == kBad) return kBad;
+  const uint64_t lim = 1 + (c + 1) * (uint64_t)kChunkB;
+  while (x < lim && x < in_len) {
+    const int L = bare_block_len<kExact>(in, in_len, x);
+    if (L == 0) return kBad;
+    if (kWrite) boff[base + cnt] = x - 1;
+    ++cnt;
+    x += (uint64_t)L;
+  }
+  return x;
+}
+
+// a lane per chunk: count and exit from the candidate, and per wave of 64
+// chunks the block count (gsum)
+template <bool kExact>
+__global__ __launch_bounds__(64) void lz4_bare_walk(const uint8_t *__restrict__ in, size_t in_len,
+                                                    size_t nchunks,
+                                                    const uint64_t *__restrict__ cand,
+                                                    uint32_t *__restrict__ cnt,
+                                                    uint64_t *__restrict__ exitp,
+                                                    unsigned long long *__restrict__ gsum) {
+  const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
+  uint32_t n = 0;
+  if (c < nchunks) {
+    exitp[c] = bare_walk_chunk<kExact, false>(in, in_len, c, cand[c], n, nullptr, 0);
+    cnt[c] = n;
+  }
+  unsigned long long t = n;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d, 64);
+  if (threadIdx.x == 0) gsum[blockIdx.x] = t;
+}
+
+// One wave: every chunk's exit must be the next chunk's candidate (and the
+// last exit the stream end).  The first chunk that breaks this is re-walked
+// from its predecessor's exit (the stream's own chain, by induction from
+// position 1) and the check resumes there.  status[0] = 0 when the chain is
+// consistent, else 1 + the chunk where it broke.
+template <bool kExact>
+__global__ __launch_bounds__(64) void lz4_bare_fix(const uint8_t *__restrict__ in, size_t in_len,
+                                                   size_t nchunks, uint64_t *__restrict__ cand,
+                                                   uint32_t *__restrict__ cnt,
+                                                   uint64_t *__restrict__ exitp,
+                                                   unsigned long long *__restrict__ gsum,
+                                                   unsigned long long *__restrict__ status) {
+  const int lane = threadIdx.x;
+  size_t ov_c = ~(size_t)0;                          // chunk re-walked last, and its exit
+  uint64_t ov_exit = 0;                              // (a later load may not see the store)
+  size_t c = 0;
+  unsigned long long st = 0;
+  while (c < nchunks) {
+    const size_t i = c + lane;
+    bool mis = false;
+    if (i < nchunks) {
+      const uint64_t e = i == ov_c ? ov_exit : exitp[i];
+      mis = i + 1 < nchunks ? e != cand[i + 1] : e != (uint64_t)in_len;
+      mis = mis || e == kBad;
+    }
+    const uint64_t m = __builtin_amdgcn_ballot_w64(mis);
+    if (!m) {
+      c += 64;
+      continue;
+    }
+    const size_t f = c + (size_t)__builtin_ctzll(m);  // first broken chunk
+    const uint64_t e = f == ov_c ? ov_exit : exitp[f];
+    if (f + 1 >= nchunks || e == kBad) {             // no way on: a corrupt stream
+      st = 1 + f;
+      break;
+    }
+    // chunk f + 1 starts where chunk f's walk left off
+    uint32_t n = 0;
+    uint64_t ex = 0;
+    if (lane == 0) ex = bare_walk_chunk<kExact, false>(in, in_len, f + 1, e, n, nullptr, 0);
+    ex = __shfl(ex, 0, 64);
+    n = (uint32_t)__shfl((int)n, 0, 64);
+    if (lane == 0) {
+      const uint32_t old = cnt[f + 1];
+      cand[f + 1] = e;
+      cnt[f + 1] = n;
+      exitp[f + 1] = ex;
+      atomicAdd(&gsum[(f + 1) / 64], (unsigned long long)n - (unsigned long long)old);
+    }
+    ov_c = f + 1;
+    ov_exit = ex;
+    c = f + 1;
+  }
+  if (lane == 0) status[0] = st;
+}
+
+// exclusive scan of the per-wave block counts (one workgroup) -> gbase; the
+// total block count -> *nb
+__global__ __launch_bounds__(1024) void lz4_bare_scan(const unsigned long long *__restrict__ gsum,
+                                                      size_t ng,
+                                                      unsigned long long *__restrict__ gbase,
+                                                      unsigned long long *__restrict__ nb) {
+  __shared__ unsigned long long ws[16];
+  __shared__ unsigned long long carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (size_t c0 = 0; c0 < ng; c0 += 1024) {
+    const size_t i = c0 + threadIdx.x;
+    const unsigned long long v = i < ng ? gsum[i] : 0;
+    unsigned long long x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long o = __shfl_up(x, d, 64);
+      if ((threadIdx.x & 63) >= d) x += o;
+    }
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = x;
+    __syncthreads();
+    unsigned long long pre = carry;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) pre += ws[w];
+    if (i < ng) gbase[i] = pre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = pre + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *nb = carry;
+}
+
+// a lane per chunk: its blocks' offsets (relative to the first block byte)
+template <bool kExact>
+__global__ __launch_bounds__(64) void lz4_bare_offsets(const uint8_t *__restrict__ in,
+                                                       size_t in_len, size_t nchunks,
+                                                       const uint64_t *__restrict__ cand,
+                                                       const uint32_t *__restrict__ cnt,
+                                                       const unsigned long long *__restrict__ gbase,
+                                                       uint64_t *__restrict__ boff) {
+  const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const uint32_t v = c < nchunks ? cnt[c] : 0u;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)x, d, 64);
+    if ((int)threadIdx.x >= d) x += o;
+  }
+  if (c >= nchunks) return;
+  const uint64_t base = gbase[blockIdx.x] + x - v;
+  uint32_t n = 0;
+  bare_walk_chunk<kExact, true>(in, in_len, c, cand[c], n, boff, base);
+}
+
 __global__ void lz4_decode_init(unsigned long long *result) {
   result[0] = 0ull;
   result[1] = ~0ull;
@@ -415,4 +672,105 @@ extern "C" int lz4r_decompress_device(const void *d_in, size_t in_len, const voi
                      static_cast<uint8_t *>(d_out), out_cap,
                      static_cast<unsigned long long *>(d_result));
   return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
+}
+
+namespace {
+
+// one pass of the bare-stream decode in mode kExact; returns LZ4R_OK, or
+// LZ4R_ERR_CORRUPT when the chain or a block does not hold together
+template <bool kExact>
+int bare_pass(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap, size_t nchunks,
+              uint64_t *cand, uint32_t *cnt, uint64_t *exitp, unsigned long long *gsum,
+              unsigned long long *gbase, unsigned long long *small, size_t *out_len,
+              hipStream_t s) {
+  const unsigned ng = (unsigned)((nchunks + 63) / 64);
+  unsigned long long *d_nb = small, *d_status = small + 1, *d_res = small + 2;
+  hipLaunchKernelGGL(lz4_bare_walk<kExact>, dim3(ng), dim3(64), 0, s, in, in_len, nchunks, cand,
+                     cnt, exitp, gsum);
+  hipLaunchKernelGGL(lz4_bare_fix<kExact>, dim3(1), dim3(64), 0, s, in, in_len, nchunks, cand, cnt,
+                     exitp, gsum, d_status);
+  hipLaunchKernelGGL(lz4_bare_scan, dim3(1), dim3(1024), 0, s, gsum, (size_t)ng, gbase, d_nb);
+  unsigned long long h[2] = {0, 0};
+  uint8_t frame = 0;
+  if (hipMemcpyAsync(h, small, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(&frame, in, 1, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return LZ4R_ERR_HIP;
+  const size_t nb = (size_t)h[0];
+  if (h[1] != 0 || nb == 0 || (uint8_t)(nb & 0xFF) != frame) return LZ4R_ERR_CORRUPT;
+  uint64_t *boff = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void **>(&boff), nb * sizeof(uint64_t), s) != hipSuccess)
+    return LZ4R_ERR_NOMEM;
+  hipLaunchKernelGGL(lz4_bare_offsets<kExact>, dim3(ng), dim3(64), 0, s, in, in_len, nchunks, cand,
+                     cnt, gbase, boff);
+  hipLaunchKernelGGL(lz4_decode_init, dim3(1), dim3(1), 0, s, d_res);
+  hipLaunchKernelGGL(lz4_decode_blocks, dim3((unsigned)((nb + kLanes - 1) / kLanes)), dim3(kLanes),
+                     0, s, in, in_len, static_cast<const uint64_t *>(boff), nb, out,
+                     out_cap, d_res);
+  (void)hipFreeAsync(boff, s);
+  unsigned long long r[2] = {0, 0};
+  if (hipMemcpyAsync(r, d_res, sizeof(r), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return LZ4R_ERR_HIP;
+  if (r[1] != ~0ull) return LZ4R_ERR_CORRUPT;
+  *out_len = (size_t)r[0];
+  return r[0] > out_cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
+}
+
+}  // namespace
+
+extern "C" int lz4r_decompress_stream_device(const void *d_in, size_t in_len, void *d_out,
+                                             size_t out_cap, size_t *out_len, void *stream) {
+  if (!d_in || !d_out || !out_len) return LZ4R_ERR_ARG;
+  *out_len = 0;
+  if (in_len < 9) return LZ4R_ERR_CORRUPT;          // a frame byte and one 8-byte block at least
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint8_t *in = static_cast<const uint8_t *>(d_in);
+  uint8_t *out = static_cast<uint8_t *>(d_out);
+  const size_t nchunks = (in_len - 1 + kChunkB - 1) / kChunkB;
+  const size_t ng = (nchunks + 63) / 64;
+  // scratch: cand, exit (u64), cnt (u32) per chunk; gsum, gbase per 64 chunks; nb, status, result
+  const size_t bytes = nchunks * 20 + ng * 16 + 4 * 8 + 64;
+  uint8_t *scr = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void **>(&scr), bytes, s) != hipSuccess) return LZ4R_ERR_NOMEM;
+  uint64_t *cand = reinterpret_cast<uint64_t *>(scr);
+  uint64_t *exitp = cand + nchunks;
+  unsigned long long *gsum = reinterpret_cast<unsigned long long *>(exitp + nchunks);
+  unsigned long long *gbase = gsum + ng;
+  unsigned long long *small = gbase + ng;
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(small + 4);
+  hipLaunchKernelGGL(lz4_bare_cand, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, in,
+                     in_len, nchunks, cand);
+  // fast mode (block length = its size field); the exact mode parses every
+  // block and is needed only for streams with truncated matches
+  int rc = bare_pass<false>(in, in_len, out, out_cap, nchunks, cand, cnt, exitp, gsum, gbase,
+                            small, out_len, s);
+  if (rc == LZ4R_ERR_CORRUPT) {
+    hipLaunchKernelGGL(lz4_bare_cand, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, in,
+                       in_len, nchunks, cand);
+    rc = bare_pass<true>(in, in_len, out, out_cap, nchunks, cand, cnt, exitp, gsum, gbase, small,
+                         out_len, s);
+  }
+  (void)hipFreeAsync(scr, s);
+  if (hipStreamSynchronize(s) != hipSuccess) return LZ4R_ERR_HIP;
+  return rc;
+}
+
+extern "C" int lz4r_decompress_stream(const uint8_t *in, size_t in_len, uint8_t *out, size_t cap,
+                                      size_t *out_len) {
+  if (!in || !out || !out_len) return LZ4R_ERR_ARG;
+  void *din = nullptr, *dout = nullptr;
+  if (hipMalloc(&din, in_len ? in_len : 1) != hipSuccess ||
+      hipMalloc(&dout, cap ? cap : 1) != hipSuccess) {
+    (void)hipFree(din);
+    return LZ4R_ERR_NOMEM;
+  }
+  int rc = hipMemcpy(din, in, in_len, hipMemcpyHostToDevice) == hipSuccess ? LZ4R_OK
+                                                                          : LZ4R_ERR_HIP;
+  if (rc == LZ4R_OK) rc = lz4r_decompress_stream_device(din, in_len, dout, cap, out_len, nullptr);
+  if (rc == LZ4R_OK && hipMemcpy(out, dout, *out_len, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = LZ4R_ERR_HIP;
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  return rc;
 }

@@ -263,15 +263,16 @@ void LZ4_decode(char *input_bin_file, char *log) {
     perror("Error: Failed to read input file");
     exit(1);
   }
-  /* every block decodes to at most 300 bytes and takes at least 5 */
-  size_t cap = (n / 5 + 1) * LZ4R_BLOCK;
+  /* every block decodes to at most 300 bytes and takes at least 8 */
+  size_t cap = (n / 8 + 1) * LZ4R_BLOCK;
   uint8_t *out = (uint8_t *)malloc(cap);
   size_t got = 0;
   if (!out) {
     perror("Error: Unable to allocate memory");
     exit(1);
   }
-  int rc = lz4r_decompress(comp, n, out, cap, &got);
+  /* on the GPU: block boundaries found on the device from the stream alone */
+  int rc = lz4r_decompress_stream(comp, n, out, cap, &got);
   if (rc != LZ4R_OK) {
     fprintf(stderr, "Error: %s\n", lz4r_strerror(rc));
     exit(1);

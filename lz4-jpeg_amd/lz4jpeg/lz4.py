@@ -207,3 +207,35 @@ def decompress_device(d_stream, length, d_offsets, nb, out_cap, d_out=None, stre
         raise Lz4Error(_lib.LZ4R_ERR_CAPACITY,
                        f"lz4r_decompress_device: needs {n} bytes, capacity {out_cap}")
     return d_out, n
+
+
+def decompress_stream_device(d_stream, length, out_cap, d_out=None, stream=None):
+    """GPU decode of a bare framed stream (lz4r_decompress_stream_device):
+    the block boundaries are found on the device, as LZ4_decode (LZ4.c:1038)
+    needs only the stream.  Returns (d_out, decoded_length); raises
+    Lz4Error(-6) on a malformed stream."""
+    import torch
+    if d_out is None:
+        d_out = torch.empty(max(out_cap, 1), dtype=torch.uint8, device=d_stream.device)
+    got = ctypes.c_size_t(0)
+    rc = _lib.lib().lz4r_decompress_stream_device(
+        ctypes.c_void_p(d_stream.data_ptr()), length, ctypes.c_void_p(d_out.data_ptr()), out_cap,
+        ctypes.byref(got), _stream_handle(stream))
+    if rc != 0:
+        _raise(rc, "lz4r_decompress_stream_device")
+    return d_out, got.value
+
+
+def decompress_stream(stream_bytes, cap=None):
+    """Host-buffer form of decompress_stream_device (lz4r_decompress_stream)."""
+    buf = np.frombuffer(bytes(stream_bytes), dtype=np.uint8)
+    if cap is None:
+        cap = (buf.size // 8 + 1) * BLOCK
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    got = ctypes.c_size_t(0)
+    rc = _lib.lib().lz4r_decompress_stream(buf.ctypes.data_as(ctypes.c_void_p), buf.size,
+                                           out.ctypes.data_as(ctypes.c_void_p), cap,
+                                           ctypes.byref(got))
+    if rc != 0:
+        _raise(rc, "lz4r_decompress_stream")
+    return out[:got.value].tobytes()
