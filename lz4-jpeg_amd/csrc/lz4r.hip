@@ -103,28 +103,28 @@ constexpr int kBlk = LZ4R_BLOCK;          // 300
 constexpr int kBlkOutMax = 560;           // >= 548: worst-case bytes of one block, 16-B multiple
 constexpr int kHB = 10;                   // hash bits: 1024 buckets
 constexpr int kH = 1 << kHB;
-constexpr int kArr = kBlk + 4;
-constexpr int kQ = kBlk;                 // walker ring (<= one live walker per entry)
+constexpr int kArr = 320;                // per-position arrays: every lane's five positions
+                                         // (p = 5 l + r <= 319) in range, no index clamps
+constexpr int kQ = kBlk + 64;            // walker queue: reads run up to 63 past the last
 constexpr int kCand = 128;               // candidate list (drained when a pass could fill it)
+static_assert(kArr >= 64 * 5, "blocked positions of all 64 lanes");
 
-// LDS of one wave (5,088 B: 32 waves per CU).  Byte offsets in TileLds::buf:
+// LDS of one wave (4,976 B: 32 waves per CU).  Byte offsets in TileLds::buf:
 //   [kInOff, +348)     the block (byte kInOff - 1 is read as blk[-1]) + an
-//                      over-read pad (lcp reads, 8-byte literal words)
-//   [kOutOff, +560)    (spare: the heads' overlay; lz4_emit writes the bytes)
-//   [kQOff, +1216)     chain walkers (q), or the slow walk's sequence starts (seq)
+//                      over-read pad (lcp reads)
+//   [kQOff, +1456)     chain walkers (q), or the slow walk's sequence starts (seq)
 //   [kCandOff, +512)   candidate pairs
 // and while the block is indexed, the 1024 u16 bucket heads overlay
-// [kHeadOff, +2048) = the output area, q and the front of cand, all of them
-// dead until the index is built.
+// [kHeadOff, +2048) = q and cand, both dead until the index is built.
 constexpr int kInOff = 16;
-constexpr int kOutOff = 368;
-constexpr int kQOff = kOutOff + kBlkOutMax;
-constexpr int kCandOff = kQOff + 4 * kArr;
-constexpr int kBufBytes = kCandOff + 4 * kCand;
-constexpr int kHeadOff = kOutOff;
-static_assert(kInOff + kBlk + 48 <= kOutOff && kOutOff % 16 == 0 && kInOff % 16 == 0 &&
+constexpr int kQOff = 368;
+constexpr int kCandOff = kQOff + 4 * kQ;
+constexpr int kHeadOff = kQOff;
+constexpr int kBufBytes = kHeadOff + 2 * kH > kCandOff + 4 * kCand ? kHeadOff + 2 * kH
+                                                                   : kCandOff + 4 * kCand;
+static_assert(kInOff + kBlk + 48 <= kQOff && kQOff % 16 == 0 && kInOff % 16 == 0 &&
                   kBlk == 75 * 4,
-              "dword staging (75 dwords), 16-B aligned output chunks");
+              "dword staging (75 dwords), aligned regions");
 static_assert(kHeadOff + 2 * kH <= kBufBytes, "heads overlay the dead regions");
 
 // scratch bytes per block slot: the header dword and <= 121 sequence records
@@ -324,13 +324,13 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = p0 + r;
-      S.rec[min(p, kArr - 1)] = 0u;     // local(p) accumulator (branch-free: past n unused)
+      S.rec[p] = 0u;                    // local(p) accumulator (branch-free: past n unused)
       const bool act = search && p < nk;
       tg[r] = (key[r] * 2654435761u) >> 17;
       const uint32_t bk = tg[r] >> (15 - kHB);
       sh[r] = (bk & 1u) << 4;
-      adr[r] = lds_off(act ? &S.head()[bk >> 1] : &S.rec[min(p, kArr - 1)]);   // inactive: own dword
-      clr[r] = act ? 0xFFFFu << sh[r] : 0u;               // inactive: a no-op swap
+      adr[r] = lds_off(&S.head()[bk >> 1]);
+      clr[r] = act ? 0xFFFFu << sh[r] : 0u;               // inactive: a no-op swap (any dword)
       set[r] = act ? ((uint32_t)p + 1u) << sh[r] : 0u;
     }
     uint32_t old[5];
@@ -342,7 +342,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       const uint32_t link = o ? o - 1u : 511u;
       const uint32_t pb = r < 4 ? (d0 >> (8 * r)) & 255u : d1 & 255u;   // blk[p - 1]
       const bool act = search && p < nk;
-      S.ent[min(p, kArr - 1)] = link | (pb << 9) | (tg[r] << 17);   // inactive: never read
+      S.ent[p] = link | (pb << 9) | (tg[r] << 17);   // inactive: never read
       item[r] = act && o ? (uint32_t)p | (link << 16) : 0u;
     }
   }
@@ -403,7 +403,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       const uint64_t em = ~vm;
       const int idx = qrd + rank_below(em);
       const uint64_t nm_ = em & ballot(idx < qwr);
-      const uint32_t it = S.q()[min(idx, kQ - 1)];
+      const uint32_t it = S.q()[idx];      // idx <= qwr + 63 < kQ
       a = (int)sel_mask(nm_, it & 0xFFFFu, (uint32_t)a);
       b = (int)sel_mask(nm_, it >> 16, (uint32_t)b);
       vm |= nm_;
@@ -436,7 +436,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     // local(p) as end << 9 | dist; 0 without a candidate and at and past n
-    v[r] = S.rec[min(p0 + r, kArr - 1)];
+    v[r] = S.rec[p0 + r];
     if (r) v[r] = max(v[r], v[r - 1]);
   }
   {
@@ -480,7 +480,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     for (int r = 4; r >= 0; --r) f[r] = (mrec[r] & 255u) ? p0 + r : f[r + 1];
 #pragma unroll
     for (int r = 0; r < 5; ++r)
-      S.nm[min(p0 + r, kArr - 1)] = f[r];   // past n: unused
+      S.nm[p0 + r] = f[r];               // past n: unused
   }
   wave_sync();
   // succ(p) = nm(p + M(p)) for the match starts; succ(n) = n.  Then the
@@ -493,8 +493,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     // branch-free: entries of positions that start no match (p = n included:
     // succ(n) = n) are written too; only their succ bits are ever read
     const int M = (int)(mrec[r] & 255u);
-    const int q = min(p0 + r, kArr - 1);
-    const int sj = (int)S.nm[min(q + M, kArr - 1)];
+    const int q = p0 + r;
+    const int sj = (int)S.nm[q + M];      // q + M <= n: matches end in the block
     j1[r] = M != 0 ? sj : n;
     S.rec[q] = mrec[r] | ((uint32_t)j1[r] << 17);
   }
@@ -507,7 +507,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int j3 = (int)(S.rec[j2[r]] >> 17);
-      S.jt[min(p0 + r, kArr - 1)] =
+      S.jt[p0 + r] =
           (uint32_t)j1[r] | ((uint32_t)j2[r] << 9) | ((uint32_t)j3 << 18);
     }
   }
@@ -575,7 +575,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     const bool ism = (int)cq < n;                                  // ends with a match
     const uint64_t mm = ballot(ism);
     const int nm_r = __popcll(mm);                                 // a prefix of the round
-    const uint32_t rv = S.rec[min(cq, (uint32_t)(kArr - 1))];
+    const uint32_t rv = S.rec[cq];        // cq <= n
     const int cpos = ism ? (int)cq : n;
     const int M = ism ? (int)(rv & 255u) : 0;
     const int D = ism ? (int)((rv >> 8) & 511u) : 0;             // the tail writes offset 0
