@@ -115,7 +115,8 @@ const char *jpegr_strerror(int code);
  *            code length << 16, in the reference's codes[] (DFS) order;
  *            the codes follow from the lengths: code[0] = 0, code[k] =
  *            (code[k-1] + 1) shifted left (or right) to length len[k]
- * d_coef 16-B aligned, d_bits 4-B aligned (JPEGR_ERR_ARG otherwise).
+ * d_coef 16-B aligned; d_bits 4-B aligned to encode, 16-B aligned to decode
+ * (JPEGR_ERR_ARG otherwise).
  * d_scratch: jpegr_entropy_scratch_bytes(ntiles) device bytes.  d_status:
  * 2 u32 on the device; [0] = streams whose code or sequence would overflow
  * the reference's char code[32] / sequence[1024|512] buffers (undefined

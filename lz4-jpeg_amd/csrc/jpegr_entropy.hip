@@ -420,14 +420,28 @@ __device__ bool decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
     const int v = (int16_t)(vl[0] & 0xFFFF);
     for (int j = 0; j < R; ++j) put(v);
   } else {
-    const uint32_t *wds = reinterpret_cast<const uint32_t *>(bits);
-    int p = 0, got = 0;
+    // MSB-first bit buffer: acc holds nacc valid bits, left-aligned; words
+    // come from 16-B chunks of the stream's slot, the next chunk in flight
+    const uint4 *src = reinterpret_cast<const uint4 *>(bits);
+    const int nch = (nbits + 127) >> 7;               // chunks holding the bits
+    uint4 q = src[0], nxt = nch > 1 ? src[1] : make_uint4(0, 0, 0, 0);
+    int qi = 0, ci = 1;
+    uint64_t acc = 0;
+    int nacc = 0, p = 0, got = 0;
     while (p < nbits) {
+      while (nacc <= 32) {                            // refill 32 bits
+        const uint32_t wd = qi == 0 ? q.x : qi == 1 ? q.y : qi == 2 ? q.z : q.w;
+        acc |= (uint64_t)__builtin_bswap32(wd) << (32 - nacc);
+        nacc += 32;
+        if (++qi == 4) {
+          qi = 0;
+          q = nxt;
+          ++ci;
+          nxt = ci < nch ? src[ci] : make_uint4(0, 0, 0, 0);
+        }
+      }
       // 32 bits at p (zero past the end)
-      const int wi = p >> 5, sh = p & 31;
-      const uint32_t w0 = __builtin_bswap32(wds[wi]);
-      const uint32_t w1 = (wi + 1) * 32 < nbits ? __builtin_bswap32(wds[wi + 1]) : 0;
-      uint32_t win = sh ? (w0 << sh) | (w1 >> (32 - sh)) : w0;
+      uint32_t win = (uint32_t)(acc >> 32);
       if (nbits - p < 32) win &= ~0u << (32 - (nbits - p));
       // largest k with lc[k] <= win
       int lo = 0, hi = U - 1;
@@ -438,9 +452,11 @@ __device__ bool decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
       }
       const uint32_t e = vl[lo];
       const int L = (int)((e >> 16) & 255);
-      if (p + L > nbits) return false;
+      if (p + L > nbits || L == 0) return false;
       put((int16_t)(e & 0xFFFF));
       p += L;
+      acc <<= L;
+      nacc -= L;
       ++got;
     }
     if (got != R) return false;
@@ -571,7 +587,7 @@ extern "C" int jpegr_entropy_decode_device(const void *d_bits, const void *d_met
                                            void *d_status, void *stream) {
   if (!d_bits || !d_meta || !d_table || !d_coef || !d_status || ntiles == 0 ||
       ntiles > ((size_t)1 << 32) / 3 || (reinterpret_cast<uintptr_t>(d_coef) & 15) != 0 ||
-      (reinterpret_cast<uintptr_t>(d_bits) & 3) != 0)
+      (reinterpret_cast<uintptr_t>(d_bits) & 15) != 0)
     return JPEGR_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (hipMemsetAsync(static_cast<uint32_t *>(d_status) + 1, 0, sizeof(uint32_t), s) != hipSuccess)
