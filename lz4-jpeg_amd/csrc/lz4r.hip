@@ -33,8 +33,7 @@
 //            uint8_t return, LZ4.c:317).
 //     parse  nm(x) = first matchable position >= x; succ(c) = nm(c + M(c));
 //            the greedy parse (LZ4.c:516-583) is the walk c0 = nm(0),
-//            c_{k+1} = succ(c_k), three sequences per LDS round trip through
-//            the jump table succ | succ^2 | succ^3.
+//            c_{k+1} = succ(c_k), one LDS read per sequence.
 //   records  sequence k on lane k: one packed wave scan of the bytes the block
 //            takes and of its size fields; record k = match start | M << 9 |
 //            dist << 17 (its literal run starts where sequence k - 1's match
@@ -137,7 +136,6 @@ struct TileLds {
   union {
     uint32_t ent[kArr];   // per position: link | preceding byte << 9 | tag << 17
     uint32_t nm[kArr];    // then: first matchable position >= x (dwords: no sub-dword LDS access)
-    uint32_t jt[kArr];    // then: succ, succ^2, succ^3 of a match start (9 bits each)
   };
   uint32_t rec[kArr];     // local(p) accumulator; then M | dist<<8 | succ<<17
   // bucket -> 1 + last inserted position (0: empty), u16 pairs (index phase)
@@ -283,8 +281,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   constexpr int base = kInOff;
 
   // ---- index: per-bucket chains of the 4-gram starts -----------------------
-  // Position p swaps itself (+1) into its bucket's head and keeps the
-  // previous head as its link.  The chains are in insertion order: rounds
+  // Position p swaps itself into its bucket's u16 head (0xFFFF = empty) and
+  // keeps the previous head as its link.  The chains are in insertion order: rounds
   // ascend, and lanes of one round that share a bucket are chained in the
   // order the LDS served their swaps.  Entry:
   //   link (9 bits, 511 = none) | preceding byte << 9 | 15-bit hash tag << 17.
@@ -297,8 +295,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   constexpr int kHeadW = kH / 2;          // head dwords (u16 heads)
   static_assert(kHeadW % 256 == 0, "head reset: 16-B stores");
 #pragma unroll
-  for (int i = 0; i < kHeadW / 256; ++i)  // empty heads (the previous block's queue)
-    reinterpret_cast<uint4 *>(S.head())[i * 64 + lane] = make_uint4(0, 0, 0, 0);
+  for (int i = 0; i < kHeadW / 256; ++i)  // empty heads (0xFFFF; the previous block's queue)
+    reinterpret_cast<uint4 *>(S.head())[i * 64 + lane] = make_uint4(~0u, ~0u, ~0u, ~0u);
   // Blocked layout: lane l owns the five positions p0 .. p0 + 4, p0 = 5 l
   // (lanes 60..63 own none of a 300-B block).  One 12-byte window per lane
   // gives all five 4-gram keys and preceding bytes; the five head swaps go
@@ -331,19 +329,19 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       sh[r] = (bk & 1u) << 4;
       adr[r] = lds_off(&S.head()[bk >> 1]);
       clr[r] = act ? 0xFFFFu << sh[r] : 0u;               // inactive: a no-op swap (any dword)
-      set[r] = act ? ((uint32_t)p + 1u) << sh[r] : 0u;
+      set[r] = act ? (uint32_t)p << sh[r] : 0u;
     }
     uint32_t old[5];
     mskor_rtn5(old, adr, clr, set);
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = p0 + r;
-      const uint32_t o = (old[r] >> sh[r]) & 0xFFFFu;
-      const uint32_t link = o ? o - 1u : 511u;
+      // the previous head (0xFFFF: none) as a 9-bit link (511: none)
+      const uint32_t link = __builtin_amdgcn_ubfe(old[r], sh[r], 9);
       const uint32_t pb = r < 4 ? (d0 >> (8 * r)) & 255u : d1 & 255u;   // blk[p - 1]
       const bool act = search && p < nk;
       S.ent[p] = link | (pb << 9) | (tg[r] << 17);   // inactive: never read
-      item[r] = act && o ? (uint32_t)p | (link << 16) : 0u;
+      item[r] = act && link != 511u ? (uint32_t)p | (link << 16) : 0u;
     }
   }
   PROF_MARK(0);                       // index
@@ -483,11 +481,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       S.nm[p0 + r] = f[r];               // past n: unused
   }
   wave_sync();
-  // succ(p) = nm(p + M(p)) for the match starts; succ(n) = n.  Then the
-  // jump table jt[p] = succ(p) | succ^2(p) << 9 | succ^3(p) << 18 (two
-  // position-parallel gathers), so the serial walk below advances three
-  // sequences per LDS round trip.
-  int j1[5];
+  // succ(p) = nm(p + M(p)) for the match starts; succ(n) = n, kept in the
+  // record word: rec[p] = M | dist << 8 | succ << 17.
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     // branch-free: entries of positions that start no match (p = n included:
@@ -495,56 +490,35 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     const int M = (int)(mrec[r] & 255u);
     const int q = p0 + r;
     const int sj = (int)S.nm[q + M];      // q + M <= n: matches end in the block
-    j1[r] = M != 0 ? sj : n;
-    S.rec[q] = mrec[r] | ((uint32_t)j1[r] << 17);
+    S.rec[q] = mrec[r] | ((uint32_t)(M != 0 ? sj : n) << 17);
   }
   const int F0 = __builtin_amdgcn_readlane(f[0], 0);    // nm(0)
   wave_sync();
-  {
-    int j2[5];
-#pragma unroll
-    for (int r = 0; r < 5; ++r) j2[r] = (int)(S.rec[j1[r]] >> 17);
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int j3 = (int)(S.rec[j2[r]] >> 17);
-      S.jt[p0 + r] =
-          (uint32_t)j1[r] | ((uint32_t)j2[r] << 9) | ((uint32_t)j3 << 18);
-    }
-  }
-  wave_sync();
 
-  PROF_MARK(4);                       // nm + jump table
+  PROF_MARK(4);                       // nm + succ
   // ---- greedy parse = walk over match starts (LZ4.c:516-583) ---------------
-  // The walk is the serial part of the block: from c0 = nm(0), each step
-  // reads the jump-table word of the last recorded start (three more starts)
-  // and keeps it in lane `it` of a register (v_writelane; reading registers
-  // with v_readlane instead of the LDS was measured 25 % slower, and every
-  // scalar instruction in this loop is paid ~25 times per block).
+  // The walk is the serial part of the block: from c0 = nm(0), c_{k+1} =
+  // succ(c_k), one LDS read per sequence; sequence k's match start is kept
+  // in lane k of a register (v_writelane).  (A jump table of succ, succ^2,
+  // succ^3 took three sequences per read but cost two position-parallel
+  // gathers; with 8 waves per SIMD the walk's latency hides behind them.)
   int c = F0, it = 0;
   uint32_t seqv = 0;
-  while (c < n) {                        // c recorded: word it = succ .. succ^3 of c
-    const uint32_t t = __builtin_amdgcn_readfirstlane(S.jt[c]);
-    // lane select = it mod 64: past 64 words (> 193 sequences) lanes are
-    // overwritten and the walk is redone below
+  while (c < n) {
+    // lane select = it mod 64: past 64 sequences lanes are overwritten and
+    // the walk is redone below
     asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
-                 : "+v"(seqv) : "s"(t), "s"(it));   // m0: not used by this kernel otherwise
+                 : "+v"(seqv) : "s"(c), "s"(it));   // m0: not used by this kernel otherwise
     ++it;
-    c = (int)(t >> 18);
+    c = (int)(__builtin_amdgcn_readfirstlane(S.rec[c]) >> 17);
   }
-  // Sequence k's match start: k = 0 -> c0, k = 1 + 3 i + f -> field f of word
-  // i (lane i of seqv), n past the last match.  Past 64 words (> 193
-  // sequences, only with truncated matches) the walk is redone into S.seq.
+  // Past 64 sequences (only with truncated matches) the walk is redone into S.seq.
   const bool slow = it > 64;
   int Sv_slow = 0;
   if (slow) {
-    if (lane == 0) S.seq()[0] = (uint32_t)F0;
-    Sv_slow = 1;
-    for (c = F0; c < n;) {
-      const uint32_t t = __builtin_amdgcn_readfirstlane(S.jt[c]);
-      const int a = (int)(t & 511u), b = (int)((t >> 9) & 511u), d = (int)(t >> 18);
-      if (lane >= 1 && lane <= 3) S.seq()[Sv_slow + lane - 1] = lane == 1 ? a : lane == 2 ? b : d;
-      Sv_slow += (a < n) + (b < n) + (d < n);
-      c = d;
+    for (c = F0; c < n; c = (int)(__builtin_amdgcn_readfirstlane(S.rec[c]) >> 17)) {
+      if (lane == 0) S.seq()[Sv_slow] = (uint32_t)c;
+      ++Sv_slow;
     }
     wave_sync();
   }
@@ -566,9 +540,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     const int kk = s0 + lane;
     uint32_t cq;
     if (!slow) {
-      const int km = kk - 1, i = (km * 21846) >> 16, f = km - 3 * i;   // km / 3 (km < 32768)
-      const uint32_t w = (uint32_t)__shfl((int)seqv, i & 63, 64);
-      cq = kk == 0 ? (uint32_t)F0 : (i < it ? (w >> (9 * f)) & 511u : (uint32_t)n);
+      cq = kk < it ? seqv : (uint32_t)n;                          // (kk < it only in round 0)
     } else {
       cq = kk < Sv_slow ? S.seq()[kk] : (uint32_t)n;
     }
