@@ -137,7 +137,7 @@ struct TileLds {
     uint32_t ent[kArr];   // per position: link | preceding byte << 9 | tag << 17
     uint32_t nm[kArr];    // then: first matchable position >= x (dwords: no sub-dword LDS access)
   };
-  uint32_t rec[kArr];     // local(p) accumulator; then M | dist<<8 | succ<<17
+  uint32_t rec[kArr];     // local(p) accumulator; then dist | M<<9 | succ<<17
   // bucket -> 1 + last inserted position (0: empty), u16 pairs (index phase)
   __device__ __forceinline__ uint32_t *head() { return reinterpret_cast<uint32_t *>(buf + kHeadOff); }
   // chain walkers, walker | next chain entry << 16 (candidate phase)
@@ -454,13 +454,18 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     }
     return 0;
   }
+  // x = v - p << 9 = len << 9 | dist (len <= 0, i.e. x < 512 or negative,
+  // where no match covers p); the record's low 17 bits are dist | M << 9 with
+  // M = len & 0xFF for len >= 4 (the uint8_t return, LZ4.c:317), else 0
   uint32_t mrec[5];
+  bool mt[5];                     // a match starts at p (M != 0)
   int f[6];                       // f[r] = first matchable position >= p0 + r
+  const uint32_t P9 = (uint32_t)p0 << 9;
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
-    const int len = (int)(v[r] >> 9) - (p0 + r);        // >= 4 iff a match starts here
-    const int M = len >= 4 ? (len & 255) : 0;           // uint8_t return, LZ4.c:317
-    mrec[r] = (uint32_t)M | ((v[r] & 511u) << 8);
+    const uint32_t x = v[r] - P9 - ((uint32_t)r << 9);
+    mrec[r] = x & ((int)x >= (4 << 9) ? 0x1FFFFu : 0x1FFu);
+    mt[r] = mrec[r] >= 512u;
   }
 
   PROF_MARK(3);                       // best scan
@@ -468,29 +473,27 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   {
     int loc = 1 << 20;            // the lane's own first matchable position
 #pragma unroll
-    for (int r = 4; r >= 0; --r) loc = (mrec[r] & 255u) ? p0 + r : loc;
+    for (int r = 4; r >= 0; --r) loc = mt[r] ? p0 + r : loc;
     const uint64_t has = ballot(loc < (1 << 20));
     const uint64_t up = has & ~((2ull << lane) - 1ull);  // lanes above this one
     const int src = up ? ctz64(up) : lane;
     const int nx = __shfl(loc, src, 64);
     f[5] = up ? nx : n;
 #pragma unroll
-    for (int r = 4; r >= 0; --r) f[r] = (mrec[r] & 255u) ? p0 + r : f[r + 1];
+    for (int r = 4; r >= 0; --r) f[r] = mt[r] ? p0 + r : f[r + 1];
 #pragma unroll
     for (int r = 0; r < 5; ++r)
       S.nm[p0 + r] = f[r];               // past n: unused
   }
   wave_sync();
-  // succ(p) = nm(p + M(p)) for the match starts; succ(n) = n, kept in the
-  // record word: rec[p] = M | dist << 8 | succ << 17.
+  // succ(p) = nm(p + M(p)) for the match starts, kept in the record word:
+  // rec[p] = dist | M << 9 | succ << 17 (branch-free: the words of positions
+  // that start no match are written too and never read)
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
-    // branch-free: entries of positions that start no match (p = n included:
-    // succ(n) = n) are written too; only their succ bits are ever read
-    const int M = (int)(mrec[r] & 255u);
     const int q = p0 + r;
-    const int sj = (int)S.nm[q + M];      // q + M <= n: matches end in the block
-    S.rec[q] = mrec[r] | ((uint32_t)(M != 0 ? sj : n) << 17);
+    const int sj = (int)S.nm[q + (int)(mrec[r] >> 9)];   // q + M <= n: matches end in the block
+    S.rec[q] = mrec[r] | ((uint32_t)sj << 17);
   }
   const int F0 = __builtin_amdgcn_readlane(f[0], 0);    // nm(0)
   wave_sync();
@@ -549,8 +552,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     const int nm_r = __popcll(mm);                                 // a prefix of the round
     const uint32_t rv = S.rec[cq];        // cq <= n
     const int cpos = ism ? (int)cq : n;
-    const int M = ism ? (int)(rv & 255u) : 0;
-    const int D = ism ? (int)((rv >> 8) & 511u) : 0;             // the tail writes offset 0
+    const int M = ism ? (int)((rv >> 9) & 255u) : 0;
+    const int D = ism ? (int)(rv & 511u) : 0;                     // the tail writes offset 0
     const int end = cpos + M;
     const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
     const int pend = lane == 0 ? end_prev : (int)upv;             // literal run start
