@@ -106,6 +106,8 @@ constexpr int kArr = 320;                // per-position arrays: every lane's fi
                                          // (p = 5 l + r <= 319) in range, no index clamps
 constexpr int kQ = kBlk + 64;            // walker queue: reads run up to 63 past the last
 constexpr int kCand = 128;               // candidate list (drained when a pass could fill it)
+constexpr uint32_t kNoLink = 2044;       // chain end: an empty head (0x07FC), a dword-aligned
+                                         // offset, so the reads past a chain's end stay aligned
 static_assert(kArr >= 64 * 5, "blocked positions of all 64 lanes");
 
 // LDS of one wave (4,976 B: 32 waves per CU).  Byte offsets in TileLds::buf:
@@ -294,9 +296,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
   constexpr int kHeadW = kH / 2;          // head dwords (u16 heads)
   static_assert(kHeadW % 256 == 0, "head reset: 16-B stores");
+  constexpr uint32_t kEmpty2 = kNoLink | (kNoLink << 16);   // two empty heads
 #pragma unroll
-  for (int i = 0; i < kHeadW / 256; ++i)  // empty heads (0xFFFF; the previous block's queue)
-    reinterpret_cast<uint4 *>(S.head())[i * 64 + lane] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  for (int i = 0; i < kHeadW / 256; ++i)  // empty heads (the previous block's queue)
+    reinterpret_cast<uint4 *>(S.head())[i * 64 + lane] = make_uint4(kEmpty2, kEmpty2, kEmpty2, kEmpty2);
   // Blocked layout: lane l owns the five positions p0 .. p0 + 4, p0 = 5 l
   // (lanes 60..63 own none of a 300-B block).  One 12-byte window per lane
   // gives all five 4-gram keys and preceding bytes; the five head swaps go
@@ -329,19 +332,23 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       sh[r] = (bk & 1u) << 4;
       adr[r] = lds_off(&S.head()[bk >> 1]);
       clr[r] = act ? 0xFFFFu << sh[r] : 0u;               // inactive: a no-op swap (any dword)
-      set[r] = act ? (uint32_t)p << sh[r] : 0u;
+      set[r] = act ? (uint32_t)(4 * p) << sh[r] : 0u;    // heads hold byte offsets 4 p
     }
     uint32_t old[5];
     mskor_rtn5(old, adr, clr, set);
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = p0 + r;
-      // the previous head (0xFFFF: none) as a 9-bit link (511: none)
-      const uint32_t link = __builtin_amdgcn_ubfe(old[r], sh[r], 9);
-      const uint32_t pb = r < 4 ? (d0 >> (8 * r)) & 255u : d1 & 255u;   // blk[p - 1]
+      // the previous head as an 11-bit byte link (kNoLink: none)
+      const uint32_t link = __builtin_amdgcn_ubfe(old[r], sh[r], 11);
+      // blk[p - 1]; 256 for p = 0, which so differs from every byte and makes
+      // every pair with j = 0 left-maximal
+      uint32_t pb = r < 4 ? (d0 >> (8 * r)) & 255u : d1 & 255u;
+      if (r == 0) pb |= lane == 0 ? 256u : 0u;
       const bool act = search && p < nk;
-      S.ent[p] = link | (pb << 9) | (tg[r] << 17);   // inactive: never read
-      item[r] = act && link != 511u ? (uint32_t)p | (link << 16) : 0u;
+      // within a bucket only the tag's low 5 bits can differ
+      S.ent[p] = link | (pb << 11) | ((tg[r] & 31u) << 20);   // inactive: never read
+      item[r] = act && link != kNoLink ? (uint32_t)(4 * p) | (link << 16) : 0u;
     }
   }
   PROF_MARK(0);                       // index
@@ -368,17 +375,22 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   PROF_MARK(1);                       // walker queue
   // ---- candidates: walk the chains ------------------------------------------
   // A pair (j < p) of one bucket is a candidate when the tags agree and the
-  // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]).  Candidates go to
+  // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]).  Walkers, links
+  // and candidates carry byte offsets 4 p into the entry arrays (no shifts
+  // per pass); entry = link | prev byte << 11 (256 at p = 0) | tag << 20.
+  // Candidates go to
   // a list in S.cand, drained by a balanced lcp pass with LDS atomicMax into
   // S.rec ((p + len) << 9 | (p - j): the longest, ties to the smallest j).
   if (search && LZ4R_VARIANT != 3) {
     constexpr int kTrash = kCand - 1;
     int ncand = 0;
+    const uint8_t *const entb = reinterpret_cast<const uint8_t *>(S.ent);
+    auto ent_at = [&](int off) { return *reinterpret_cast<const uint32_t *>(entb + off); };
     auto drain = [&]() {
       wave_sync();
       for (int i = lane; i < ncand && LZ4R_VARIANT != 4; i += 64) {
         const uint32_t pr = S.cand()[i];
-        const int p = (int)(pr & 0xFFFFu), j = (int)(pr >> 16);
+        const int p = (int)(pr & 0xFFFFu) >> 2, j = (int)(pr >> 18);
         const int l = lcp(S.buf, base + j, base + p, n - p);
         // (end, dist) as the best scan wants it: for one p the larger end is
         // the longer match and the larger dist the smaller source
@@ -394,30 +406,34 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     // loop-carried bool costs two VALU (v_cndmask + v_cmp) per use, and the
     // selects take the mask straight from SGPRs (every mask here is last
     // written by a SALU op: no VALU-SGPR hazard)
-    int qrd = 0;
+    // queue and candidate positions as byte offsets (4 i): one v_lshl_add each
+    int qrd4 = 0;
+    const int qwr4 = 4 * qwr;
+    const uint8_t *const qb = reinterpret_cast<const uint8_t *>(S.q());
+    uint8_t *const cb = reinterpret_cast<uint8_t *>(S.cand());
     int a = 0, b = 0;
     uint64_t vm = 0;                       // lanes holding a walker
     for (;;) {
       const uint64_t em = ~vm;
-      const int idx = qrd + rank_below(em);
-      const uint64_t nm_ = em & ballot(idx < qwr);
-      const uint32_t it = S.q()[idx];      // idx <= qwr + 63 < kQ
+      const int idx4 = qrd4 + (rank_below(em) << 2);
+      const uint64_t nm_ = em & ballot(idx4 < qwr4);
+      const uint32_t it = *reinterpret_cast<const uint32_t *>(qb + idx4);   // idx <= qwr + 63 < kQ
       a = (int)sel_mask(nm_, it & 0xFFFFu, (uint32_t)a);
       b = (int)sel_mask(nm_, it >> 16, (uint32_t)b);
       vm |= nm_;
       if (vm == 0) break;                  // no walker left and the queue is empty
-      qrd += __popcll(em);
-      const uint32_t me = S.ent[a], o = S.ent[b];
+      qrd4 += 4 * __popcll(em);
+      const uint32_t me = ent_at(a), o = ent_at(b);
       const uint32_t x = me ^ o;
       const int p = max(a, b), j = min(a, b);
       // a ballot of each compare (a ballot of a combined bool costs two VALU)
-      const uint64_t cm =
-          vm & ballot((x >> 17) == 0) & (ballot(j == 0) | ballot((x & (255u << 9)) != 0));
-      const int sl = (int)sel_mask(cm, (uint32_t)(ncand + rank_below(cm)), (uint32_t)kTrash);
-      S.cand()[sl] = (uint32_t)p | ((uint32_t)j << 16);
+      const uint64_t cm = vm & ballot((x >> 20) == 0) & ballot((x & (511u << 11)) != 0);
+      const int sl4 =
+          (int)sel_mask(cm, (uint32_t)(4 * ncand + (rank_below(cm) << 2)), (uint32_t)(4 * kTrash));
+      *reinterpret_cast<uint32_t *>(cb + sl4) = (uint32_t)p | ((uint32_t)j << 16);
       ncand += __popcll(cm);
-      b = (int)(o & 511u);
-      vm &= ballot(b != 511);
+      b = (int)(o & 2047u);
+      vm &= ballot(b != (int)kNoLink);
       if (ncand > kTrash - 64) {
         drain();
         ncand = 0;
