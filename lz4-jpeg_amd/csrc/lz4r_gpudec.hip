@@ -441,7 +441,8 @@ __device__ __forceinline__ int rd_u16(const uint8_t *w, int a) {
 __global__ __launch_bounds__(256) void lz4_bare_cand(const uint8_t *__restrict__ in,
                                                       size_t in_len, size_t nchunks,
                                                       uint64_t *__restrict__ cand) {
-  __shared__ alignas(16) uint8_t win[4][kWin + 16];
+  constexpr int kWin16 = (kWin + 16 + 15) / 16;       // 16-B pieces of the window
+  __shared__ alignas(16) uint8_t win[4][kWin16 * 16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const size_t c = (size_t)blockIdx.x * 4 + wv;
   if (c >= nchunks) return;
@@ -450,8 +451,23 @@ __global__ __launch_bounds__(256) void lz4_bare_cand(const uint8_t *__restrict__
     return;
   }
   const size_t s = 1 + c * (size_t)kChunkB;
-  uint8_t *w = win[wv];
-  for (int i = lane; i < kWin; i += 64) w[i] = s + i < in_len ? in[s + i] : 0;
+  // the window [s, s + kWin) as aligned 16-B loads from s & ~15 (pieces
+  // past the stream end bytewise, zero-filled)
+  const size_t a0 = s & ~(size_t)15;
+  uint8_t *const w = win[wv] + (s - a0);            // w[i] = in[s + i]
+  for (int k = lane; k < kWin16; k += 64) {
+    const size_t at = a0 + 16 * (size_t)k;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (at + 16 <= in_len) {
+      v = *reinterpret_cast<const uint4 *>(in + at);
+    } else {
+      uint32_t t[4] = {0, 0, 0, 0};
+      for (int b = 0; b < 16; ++b)
+        if (at + b < in_len) t[b >> 2] |= (uint32_t)in[at + b] << (8 * (b & 3));
+      v = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+    reinterpret_cast<uint4 *>(win[wv])[k] = v;
+  }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const int avail = (int)min((size_t)kWin, in_len - s);   // window bytes inside the stream
@@ -540,38 +556,78 @@ __global__ __launch_bounds__(64) void lz4_bare_walk(const uint8_t *__restrict__ 
   if (threadIdx.x == 0) gsum[blockIdx.x] = t;
 }
 
-// One wave: every chunk's exit must be the next chunk's candidate (and the
-// last exit the stream end).  The first chunk that breaks this is re-walked
-// from its predecessor's exit (the stream's own chain, by induction from
-// position 1) and the check resumes there.  status[0] = 0 when the chain is
-// consistent, else 1 + the chunk where it broke.
+// A lane per chunk: chunk c is consistent when its exit is the next chunk's
+// candidate (the last chunk's: the stream end).  The inconsistent ones go to
+// an unordered list (count in *nmis; the list holds at most kMisCap).
+constexpr int kMisCap = 1024;
+__global__ __launch_bounds__(256) void lz4_bare_check(size_t in_len, size_t nchunks,
+                                                      const uint64_t *__restrict__ cand,
+                                                      const uint64_t *__restrict__ exitp,
+                                                      unsigned int *__restrict__ nmis,
+                                                      unsigned int *__restrict__ mis) {
+  const size_t c = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= nchunks) return;
+  const uint64_t e = exitp[c];
+  const bool bad = e == kBad || (c + 1 < nchunks ? e != cand[c + 1] : e != (uint64_t)in_len);
+  if (bad) {
+    const unsigned int k = atomicAdd(nmis, 1u);
+    if (k < (unsigned)kMisCap) mis[k] = (unsigned int)c;
+  }
+}
+
+// One wave, in stream order over the listed chunks: a chunk whose exit is
+// not the next chunk's candidate has the next chunk re-walked from that exit
+// (the stream's own chain, by induction from position 1), which is then
+// checked in turn; the others keep what lz4_bare_walk found.  More than
+// kMisCap inconsistent chunks: every chunk is checked in order.
+// status[0] = 0 when the chain is consistent, else 1 + the chunk where it broke.
 template <bool kExact>
 __global__ __launch_bounds__(64) void lz4_bare_fix(const uint8_t *__restrict__ in, size_t in_len,
                                                    size_t nchunks, uint64_t *__restrict__ cand,
                                                    uint32_t *__restrict__ cnt,
                                                    uint64_t *__restrict__ exitp,
                                                    unsigned long long *__restrict__ gsum,
+                                                   const unsigned int *__restrict__ nmis_p,
+                                                   const unsigned int *__restrict__ mis,
                                                    unsigned long long *__restrict__ status) {
+  __shared__ unsigned int list[kMisCap];
   const int lane = threadIdx.x;
+  const unsigned int nmis = *nmis_p;
+  const bool all = nmis > (unsigned)kMisCap;         // too many: check every chunk
+  const int nl = all ? 0 : (int)nmis;
+  for (int i = lane; i < nl; i += 64) list[i] = mis[i];
+  __syncthreads();
   size_t ov_c = ~(size_t)0;                          // chunk re-walked last, and its exit
   uint64_t ov_exit = 0;                              // (a later load may not see the store)
-  size_t c = 0;
+  size_t pos = 0;                                    // chunks below pos are consistent
+  size_t force = ~(size_t)0;                         // a re-walked chunk, checked next
   unsigned long long st = 0;
-  while (c < nchunks) {
-    const size_t i = c + lane;
-    bool mis = false;
-    if (i < nchunks) {
-      const uint64_t e = i == ov_c ? ov_exit : exitp[i];
-      mis = i + 1 < nchunks ? e != cand[i + 1] : e != (uint64_t)in_len;
-      mis = mis || e == kBad;
+  for (;;) {
+    size_t f;
+    if (force != ~(size_t)0) {
+      f = force;
+    } else if (all) {
+      f = pos;                                       // (slow path: every chunk in order)
+    } else {
+      size_t m = ~(size_t)0;                         // smallest listed chunk >= pos
+      for (int i = lane; i < nl; i += 64)
+        if (list[i] >= pos && list[i] < m) m = list[i];
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        const size_t o = __shfl_xor(m, d, 64);
+        m = o < m ? o : m;
+      }
+      f = m;
     }
-    const uint64_t m = __builtin_amdgcn_ballot_w64(mis);
-    if (!m) {
-      c += 64;
+    if (f >= nchunks) break;
+    force = ~(size_t)0;
+    const uint64_t e = f == ov_c ? ov_exit : exitp[f];
+    const bool bad =
+        e == kBad || (f + 1 < nchunks ? e != cand[f + 1] : e != (uint64_t)in_len);
+    if (!bad) {
+      pos = f + 1;
       continue;
     }
-    const size_t f = c + (size_t)__builtin_ctzll(m);  // first broken chunk
-    const uint64_t e = f == ov_c ? ov_exit : exitp[f];
     if (f + 1 >= nchunks || e == kBad) {             // no way on: a corrupt stream
       st = 1 + f;
       break;
@@ -591,7 +647,8 @@ __global__ __launch_bounds__(64) void lz4_bare_fix(const uint8_t *__restrict__ i
     }
     ov_c = f + 1;
     ov_exit = ex;
-    c = f + 1;
+    pos = f + 1;
+    force = f + 1;
   }
   if (lane == 0) status[0] = st;
 }
@@ -685,10 +742,15 @@ int bare_pass(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap, si
               hipStream_t s) {
   const unsigned ng = (unsigned)((nchunks + 63) / 64);
   unsigned long long *d_nb = small, *d_status = small + 1, *d_res = small + 2;
+  unsigned int *nmis = reinterpret_cast<unsigned int *>(small + 4);
+  unsigned int *mis = reinterpret_cast<unsigned int *>(small + 5);
   hipLaunchKernelGGL(lz4_bare_walk<kExact>, dim3(ng), dim3(64), 0, s, in, in_len, nchunks, cand,
                      cnt, exitp, gsum);
+  if (hipMemsetAsync(nmis, 0, sizeof(unsigned int), s) != hipSuccess) return LZ4R_ERR_HIP;
+  hipLaunchKernelGGL(lz4_bare_check, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s,
+                     in_len, nchunks, cand, exitp, nmis, mis);
   hipLaunchKernelGGL(lz4_bare_fix<kExact>, dim3(1), dim3(64), 0, s, in, in_len, nchunks, cand, cnt,
-                     exitp, gsum, d_status);
+                     exitp, gsum, nmis, mis, d_status);
   hipLaunchKernelGGL(lz4_bare_scan, dim3(1), dim3(1024), 0, s, gsum, (size_t)ng, gbase, d_nb);
   unsigned long long h[2] = {0, 0};
   uint8_t frame = 0;
@@ -729,8 +791,9 @@ extern "C" int lz4r_decompress_stream_device(const void *d_in, size_t in_len, vo
   uint8_t *out = static_cast<uint8_t *>(d_out);
   const size_t nchunks = (in_len - 1 + kChunkB - 1) / kChunkB;
   const size_t ng = (nchunks + 63) / 64;
-  // scratch: cand, exit (u64), cnt (u32) per chunk; gsum, gbase per 64 chunks; nb, status, result
-  const size_t bytes = nchunks * 20 + ng * 16 + 4 * 8 + 64;
+  // scratch: cand, exit (u64), cnt (u32) per chunk; gsum, gbase per 64 chunks; nb, status,
+  // result[2], the inconsistent-chunk count and list (kMisCap u32)
+  const size_t bytes = nchunks * 20 + ng * 16 + 5 * 8 + 4 * (size_t)kMisCap + 64;
   uint8_t *scr = nullptr;
   if (hipMallocAsync(reinterpret_cast<void **>(&scr), bytes, s) != hipSuccess) return LZ4R_ERR_NOMEM;
   uint64_t *cand = reinterpret_cast<uint64_t *>(scr);
@@ -738,7 +801,7 @@ extern "C" int lz4r_decompress_stream_device(const void *d_in, size_t in_len, vo
   unsigned long long *gsum = reinterpret_cast<unsigned long long *>(exitp + nchunks);
   unsigned long long *gbase = gsum + ng;
   unsigned long long *small = gbase + ng;
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(small + 4);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(small + 5 + kMisCap / 2);
   hipLaunchKernelGGL(lz4_bare_cand, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, in,
                      in_len, nchunks, cand);
   // fast mode (block length = its size field); the exact mode parses every

@@ -1,5 +1,7 @@
 """Compress the bench corpus once, then run the GPU decoder a few times (for
-profilers), on the compressor's device-resident block offsets."""
+profilers), on the compressor's device-resident block offsets, and the
+bare-stream decode (block boundaries found on the device) as often."""
+import time
 import os
 import sys
 
@@ -25,4 +27,10 @@ for _ in range(reps):
     print(f"decode ms {e0.elapsed_time(e1):.3f}", flush=True)
 _, got = lz4.decompress_device(d_stream, length, d_offs, nb, n + 300, d_out=d_out)
 print("ok", got == n and bool(torch.equal(d_out[:n], d_in)))
+for _ in range(reps):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, got = lz4.decompress_stream_device(d_stream, length, n + 300, d_out=d_out)
+    print(f"bare-stream call ms {(time.perf_counter() - t0) * 1e3:.3f}", flush=True)
+print("bare ok", got == n and bool(torch.equal(d_out[:n], d_in)))
 c.close()
