@@ -390,7 +390,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       wave_sync();
       for (int i = lane; i < ncand && LZ4R_VARIANT != 4; i += 64) {
         const uint32_t pr = S.cand()[i];
-        const int p = (int)(pr & 0xFFFFu) >> 2, j = (int)(pr >> 18);
+        const int ea = (int)(pr & 0xFFFFu) >> 2, eb = (int)(pr >> 18);
+        const int p = max(ea, eb), j = min(ea, eb);
         const int l = lcp(S.buf, base + j, base + p, n - p);
         // (end, dist) as the best scan wants it: for one p the larger end is
         // the longer match and the larger dist the smaller source
@@ -414,23 +415,25 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     int a = 0, b = 0;
     uint64_t vm = 0;                       // lanes holding a walker
     for (;;) {
-      const uint64_t em = ~vm;
-      const int idx4 = qrd4 + (rank_below(em) << 2);
-      const uint64_t nm_ = em & ballot(idx4 < qwr4);
-      const uint32_t it = *reinterpret_cast<const uint32_t *>(qb + idx4);   // idx <= qwr + 63 < kQ
-      a = (int)sel_mask(nm_, it & 0xFFFFu, (uint32_t)a);
-      b = (int)sel_mask(nm_, it >> 16, (uint32_t)b);
-      vm |= nm_;
+      if (qrd4 < qwr4) {                   // (uniform) idle lanes take queued walkers
+        const uint64_t em = ~vm;
+        const int idx4 = qrd4 + (rank_below(em) << 2);
+        const uint64_t nm_ = em & ballot(idx4 < qwr4);
+        const uint32_t it = *reinterpret_cast<const uint32_t *>(qb + idx4);   // idx <= qwr + 63 < kQ
+        a = (int)sel_mask(nm_, it & 0xFFFFu, (uint32_t)a);
+        b = (int)sel_mask(nm_, it >> 16, (uint32_t)b);
+        vm |= nm_;
+        qrd4 += 4 * __popcll(em);
+      }
       if (vm == 0) break;                  // no walker left and the queue is empty
-      qrd4 += 4 * __popcll(em);
       const uint32_t me = ent_at(a), o = ent_at(b);
       const uint32_t x = me ^ o;
-      const int p = max(a, b), j = min(a, b);
       // a ballot of each compare (a ballot of a combined bool costs two VALU)
       const uint64_t cm = vm & ballot((x >> 20) == 0) & ballot((x & (511u << 11)) != 0);
       const int sl4 =
           (int)sel_mask(cm, (uint32_t)(4 * ncand + (rank_below(cm) << 2)), (uint32_t)(4 * kTrash));
-      *reinterpret_cast<uint32_t *>(cb + sl4) = (uint32_t)p | ((uint32_t)j << 16);
+      // the pair as walked (walker, chain entry): the drain orders it
+      *reinterpret_cast<uint32_t *>(cb + sl4) = (uint32_t)a | ((uint32_t)b << 16);
       ncand += __popcll(cm);
       b = (int)(o & 2047u);
       vm &= ballot(b != (int)kNoLink);
