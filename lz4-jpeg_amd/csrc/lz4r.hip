@@ -321,18 +321,20 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
                              __builtin_amdgcn_alignbyte(d1, d0, 2u),
                              __builtin_amdgcn_alignbyte(d1, d0, 3u), d1,
                              __builtin_amdgcn_alignbyte(d2, d1, 1u)};
-    uint32_t adr[5], clr[5], set[5], sh[5], tg[5];
+    uint32_t adr[5], clr[5], set[5], sh[5], hv[5];
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = p0 + r;
       S.rec[p] = 0u;                    // local(p) accumulator (branch-free: past n unused)
       const bool act = search && p < nk;
-      tg[r] = (key[r] * 2654435761u) >> 17;
-      const uint32_t bk = tg[r] >> (15 - kHB);
+      hv[r] = key[r] * 2654435761u;             // bucket = top 10 bits, tag = the next 5
+      const uint32_t bk = hv[r] >> (32 - kHB);
       sh[r] = (bk & 1u) << 4;
-      adr[r] = lds_off(&S.head()[bk >> 1]);
-      clr[r] = act ? 0xFFFFu << sh[r] : 0u;               // inactive: a no-op swap (any dword)
-      set[r] = act ? (uint32_t)(4 * p) << sh[r] : 0u;    // heads hold byte offsets 4 p
+      // inactive positions swap into their own entry dword, written after the
+      // swaps (distinct addresses: no serialised same-address atomics)
+      adr[r] = act ? lds_off(&S.head()[bk >> 1]) : lds_off(&S.ent[p]);
+      clr[r] = 0xFFFFu << sh[r];
+      set[r] = (uint32_t)(4 * p) << sh[r];               // heads hold byte offsets 4 p
     }
     uint32_t old[5];
     mskor_rtn5(old, adr, clr, set);
@@ -347,7 +349,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       if (r == 0) pb |= lane == 0 ? 256u : 0u;
       const bool act = search && p < nk;
       // within a bucket only the tag's low 5 bits can differ
-      S.ent[p] = link | (pb << 11) | ((tg[r] & 31u) << 20);   // inactive: never read
+      S.ent[p] = link | (hv[r] & (31u << 17)) | (pb << 22);   // inactive: never read
       item[r] = act && link != kNoLink ? (uint32_t)(4 * p) | (link << 16) : 0u;
     }
   }
@@ -377,7 +379,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   // A pair (j < p) of one bucket is a candidate when the tags agree and the
   // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]).  Walkers, links
   // and candidates carry byte offsets 4 p into the entry arrays (no shifts
-  // per pass); entry = link | prev byte << 11 (256 at p = 0) | tag << 20.
+  // per pass); entry = link | tag << 17 | prev byte << 22 (256 at p = 0).
   // Candidates go to
   // a list in S.cand, drained by a balanced lcp pass with LDS atomicMax into
   // S.rec ((p + len) << 9 | (p - j): the longest, ties to the smallest j).
@@ -429,7 +431,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
       const uint32_t me = ent_at(a), o = ent_at(b);
       const uint32_t x = me ^ o;
       // a ballot of each compare (a ballot of a combined bool costs two VALU)
-      const uint64_t cm = vm & ballot((x >> 20) == 0) & ballot((x & (511u << 11)) != 0);
+      const uint64_t cm = vm & ballot((x & (31u << 17)) == 0) & ballot(x >= (1u << 22));
       const int sl4 =
           (int)sel_mask(cm, (uint32_t)(4 * ncand + (rank_below(cm) << 2)), (uint32_t)(4 * kTrash));
       // the pair as walked (walker, chain entry): the drain orders it
