@@ -50,7 +50,7 @@ extern "C" {
 #define LZ4R_ERR_CORRUPT (-6)     /* decoder: malformed stream */
 
 /* Inputs up to 2^40 bytes per call; the kernels run in chunks of 2^24 blocks
- * (5.03 GB), so device scratch is ~9.4 GB of block slots at most plus
+ * (5.03 GB), so device scratch is ~10.7 GB of block slots at most plus
  * 16 B per block of the whole input. */
 
 typedef struct lz4r_ctx lz4r_ctx;

@@ -128,8 +128,10 @@ static_assert(kInOff + kBlk + 48 <= kQOff && kQOff % 16 == 0 && kInOff % 16 == 0
               "dword staging (75 dwords), aligned regions");
 static_assert(kHeadOff + 2 * kH <= kBufBytes, "heads overlay the dead regions");
 
-// scratch bytes per block slot: the header dword and <= 121 sequence records
-constexpr int kSlot = 560;
+// scratch bytes per block slot: the header dword and <= 121 sequence records;
+// 5 x 128 B, so a block's record head (the 128 B lz4_emit stages) is one L2
+// line, not two (560-B slots straddled a line boundary 7 times in 8)
+constexpr int kSlot = 640;
 static_assert(kSlot % 16 == 0 && kSlot >= kBlkOutMax && kBlkOutMax / 16 <= 64,
               "aligned slots, one store round");
 
@@ -971,7 +973,7 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
 // grid may not exceed 2^32 work-items, so a call is cut into chunks of at
 // most kChunk blocks (5.03 GB of input; a multiple of the scan partial, so
 // every chunk starts on a gather group and a partial).  The block slots are
-// sized for one chunk (9.4 GB at most) and reused; the per-block arrays and
+// sized for one chunk (10.7 GB at most) and reused; the per-block arrays and
 // the scan state span the whole call.  Each chunk is a full compress ->
 // scan -> gather pass that continues the stream offset the previous chunk
 // left in *d_len; the per-chunk launch cost (four launches) is noise against
