@@ -482,7 +482,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   // M = len & 0xFF for len >= 4 (the uint8_t return, LZ4.c:317), else 0
   uint32_t mrec[5];
   bool mt[5];                     // a match starts at p (M != 0)
-  int f[6];                       // f[r] = first matchable position >= p0 + r
+  int f[6];                       // f[r] = 4 x the first matchable position >= p0 + r
   const uint32_t P9 = (uint32_t)p0 << 9;
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
@@ -493,25 +493,27 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
 
   PROF_MARK(3);                       // best scan
   // ---- nm(x): first matchable position >= x, for x in [0, n] ---------------
+  // (as byte offsets 4 x: the serial walk then addresses the record words
+  // without a scalar shift per sequence)
   {
     int loc = 1 << 20;            // the lane's own first matchable position
 #pragma unroll
-    for (int r = 4; r >= 0; --r) loc = mt[r] ? p0 + r : loc;
+    for (int r = 4; r >= 0; --r) loc = mt[r] ? 4 * (p0 + r) : loc;
     const uint64_t has = ballot(loc < (1 << 20));
     const uint64_t up = has & ~((2ull << lane) - 1ull);  // lanes above this one
     const int src = up ? ctz64(up) : lane;
     const int nx = __shfl(loc, src, 64);
-    f[5] = up ? nx : n;
+    f[5] = up ? nx : 4 * n;
 #pragma unroll
-    for (int r = 4; r >= 0; --r) f[r] = mt[r] ? p0 + r : f[r + 1];
+    for (int r = 4; r >= 0; --r) f[r] = mt[r] ? 4 * (p0 + r) : f[r + 1];
 #pragma unroll
     for (int r = 0; r < 5; ++r)
       S.nm[p0 + r] = f[r];               // past n: unused
   }
   wave_sync();
   // succ(p) = nm(p + M(p)) for the match starts, kept in the record word:
-  // rec[p] = dist | M << 9 | succ << 17 (branch-free: the words of positions
-  // that start no match are written too and never read)
+  // rec[p] = dist | M << 9 | 4 succ << 17 (branch-free: the words of
+  // positions that start no match are written too and never read)
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     const int q = p0 + r;
@@ -528,22 +530,29 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   // in lane k of a register (v_writelane).  (A jump table of succ, succ^2,
   // succ^3 took three sequences per read but cost two position-parallel
   // gathers; with 8 waves per SIMD the walk's latency hides behind them.)
-  int c = F0, it = 0;
+  // (c4 = 4 c, the record word's byte offset)
+  const uint8_t *const recb = reinterpret_cast<const uint8_t *>(S.rec);
+  auto succ4 = [&](int c4) {
+    return (int)(__builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t *>(recb + c4)) >>
+                 17);
+  };
+  const int n4 = 4 * n;
+  int c4 = F0, it = 0;
   uint32_t seqv = 0;
-  while (c < n) {
+  while (c4 < n4) {
     // lane select = it mod 64: past 64 sequences lanes are overwritten and
     // the walk is redone below
     asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
-                 : "+v"(seqv) : "s"(c), "s"(it));   // m0: not used by this kernel otherwise
+                 : "+v"(seqv) : "s"(c4), "s"(it));   // m0: the lane select (one SGPR read per VOP3)
     ++it;
-    c = (int)(__builtin_amdgcn_readfirstlane(S.rec[c]) >> 17);
+    c4 = succ4(c4);
   }
   // Past 64 sequences (only with truncated matches) the walk is redone into S.seq.
   const bool slow = it > 64;
   int Sv_slow = 0;
   if (slow) {
-    for (c = F0; c < n; c = (int)(__builtin_amdgcn_readfirstlane(S.rec[c]) >> 17)) {
-      if (lane == 0) S.seq()[Sv_slow] = (uint32_t)c;
+    for (c4 = F0; c4 < n4; c4 = succ4(c4)) {
+      if (lane == 0) S.seq()[Sv_slow] = (uint32_t)c4 >> 2;
       ++Sv_slow;
     }
     wave_sync();
@@ -566,7 +575,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     const int kk = s0 + lane;
     uint32_t cq;
     if (!slow) {
-      cq = kk < it ? seqv : (uint32_t)n;                          // (kk < it only in round 0)
+      cq = kk < it ? seqv >> 2 : (uint32_t)n;                     // (kk < it only in round 0)
     } else {
       cq = kk < Sv_slow ? S.seq()[kk] : (uint32_t)n;
     }
