@@ -841,8 +841,7 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   }
   __syncthreads();
   const uint64_t G0 = toff[h0];
-  const uintptr_t abs0 = (uintptr_t)(out + G0);
-  const int lead = (int)(abs0 & 15);               // img[lead] = stream byte G0
+  const int lead = (int)(((uintptr_t)out + G0) & 15);   // img[lead] = stream byte G0
   // ---- records -> bytes: wave wv takes blocks [bl0, bl1) ------------------------
   {
     constexpr int kBW = kGH / kEW;                   // blocks per wave
@@ -956,21 +955,23 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   // ---- LDS image -> stream (aligned 16-B stores) --------------------------------
   const uint64_t G1 = min(toff[h1], cap);
   if (G1 <= G0) return;
-  const uintptr_t absend = (uintptr_t)(out + G1);
-  const uintptr_t first = abs0 & ~(uintptr_t)15;
-  const int nchunks = (int)((absend - first + 15) >> 4);
+  // chunk ci covers stream bytes [F + 16 ci, F + 16 ci + 16), F = G0 - lead
+  // (16-B aligned): offsets from `out`, so the stores stay global_store (a
+  // pointer rebuilt from an integer is a flat address: every flat store also
+  // counts in lgkmcnt and serialised this loop behind its LDS reads)
+  const uint64_t F = G0 - (uint64_t)lead;
+  const int nchunks = (int)((G1 - F + 15) >> 4);
   for (int ci = tid; ci < nchunks; ci += 64 * kEW) {
-    const uintptr_t a = first + ((uintptr_t)ci << 4);
+    const uint64_t a = F + ((uint64_t)ci << 4);
     const uint4 v = reinterpret_cast<const uint4 *>(img)[ci];
-    if (a >= abs0 && a + 16 <= absend) {
-      *reinterpret_cast<uint4 *>(a) = v;
+    if (a >= G0 && a + 16 <= G1) {
+      *reinterpret_cast<uint4 *>(out + a) = v;
     } else {
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int b = 0; b < 16; ++b) {
-        const uintptr_t ab = a + b;
-        if (ab >= abs0 && ab < absend)
-          *reinterpret_cast<uint8_t *>(ab) = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        const uint64_t ab = a + b;
+        if (ab >= G0 && ab < G1) out[ab] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
       }
     }
   }
