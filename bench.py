@@ -413,6 +413,11 @@ def run_lz4(ctx, n_total, scaling):
         "achieved": round(n / (avg_match_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
         "unit": "GB/s", "frac": round(n / (avg_match_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
         "traffic": measured_traffic("lz4", n, 1 << 30),
+        # HBM bytes of the whole compressor (lz4_tiles + lz4_emit) per call; the
+        # call's algorithmic bytes are 1 B read + ~1.035 B written per input byte
+        "pipeline_traffic": (None if measured_traffic("lz4_emit", n, 1 << 30) is None else
+                             measured_traffic("lz4", n, 1 << 30) +
+                             measured_traffic("lz4_emit", n, 1 << 30)),
         "binding_roof": issue_roof(n, avg_match_ms),
         "algorithmic_bytes_per_launch": n,
         "avg_launch_ms": round(avg_match_ms, 4),
