@@ -13,10 +13,10 @@
 // kernel lives on).  Per block:
 //   stage    the block's 75 dwords -> LDS (the only read of the input).
 //   position-parallel, blocked (lane l owns p = 5 l .. 5 l + 4):
-//     index  per-bucket chains of the 4-gram starts by a 10-bit hash: p swaps
-//            itself into its bucket's u16 head (ds_mskor_rtn_b32 on a dword of
-//            two heads) and keeps the old head as its link;
-//            entry = link | preceding byte << 9 | tag << 17.
+//     index  per-bucket chains of the 4-gram starts by a 10-bit hash: p
+//            exchanges itself into its bucket's u32 head (ds_wrxchg_rtn_b32)
+//            and keeps the old head as its link (byte offsets 4 p);
+//            entry = link | tag << 17 | preceding byte << 22.
 //     local  every unordered pair of a bucket is met once, by the later-
 //            inserted entry walking its chain; a lane keeps its walker until
 //            the chain ends and then takes the next queued one.  A pair
@@ -115,8 +115,10 @@ static_assert(kArr >= 64 * 5, "blocked positions of all 64 lanes");
 //                      over-read pad (lcp reads)
 //   [kQOff, +1456)     chain walkers (q), or the slow walk's sequence starts (seq)
 //   [kCandOff, +512)   candidate pairs
-// and while the block is indexed, the 1024 u16 bucket heads overlay
-// [kHeadOff, +2048) = q and cand, both dead until the index is built.
+// then ent[320] and rec[320].  While the block is indexed, the 1024 u32
+// bucket heads overlay [kHeadOff, +4096) = q, cand, ent and rec[0..192), all
+// dead until the index is built (ent and rec are written after the heads'
+// last exchange).
 constexpr int kInOff = 16;
 constexpr int kQOff = 368;
 constexpr int kCandOff = kQOff + 4 * kQ;
@@ -126,7 +128,6 @@ constexpr int kBufBytes = kHeadOff + 2 * kH > kCandOff + 4 * kCand ? kHeadOff + 
 static_assert(kInOff + kBlk + 48 <= kQOff && kQOff % 16 == 0 && kInOff % 16 == 0 &&
                   kBlk == 75 * 4,
               "dword staging (75 dwords), aligned regions");
-static_assert(kHeadOff + 2 * kH <= kBufBytes, "heads overlay the dead regions");
 
 // scratch bytes per block slot: the header dword and <= 121 sequence records;
 // 5 x 128 B, so a block's record head (the 128 B lz4_emit stages) is one L2
@@ -142,8 +143,6 @@ struct TileLds {
     uint32_t nm[kArr];    // then: first matchable position >= x (dwords: no sub-dword LDS access)
   };
   uint32_t rec[kArr];     // local(p) accumulator; then dist | M<<9 | succ<<17
-  // bucket -> 1 + last inserted position (0: empty), u16 pairs (index phase)
-  __device__ __forceinline__ uint32_t *head() { return reinterpret_cast<uint32_t *>(buf + kHeadOff); }
   // chain walkers, walker | next chain entry << 16 (candidate phase)
   __device__ __forceinline__ uint32_t *q() { return reinterpret_cast<uint32_t *>(buf + kQOff); }
   // per sequence, its match start (slow walk only)
@@ -152,28 +151,32 @@ struct TileLds {
   __device__ __forceinline__ uint32_t *cand() { return reinterpret_cast<uint32_t *>(buf + kCandOff); }
 };
 
+constexpr int kEntOff = kBufBytes;              // byte offsets of ent and rec in TileLds
+constexpr int kRecOff = kBufBytes + 4 * kArr;
+static_assert(kHeadOff + 4 * kH <= kRecOff + 4 * 192, "u32 heads end before rec[192]");
+static_assert(kRecOff + 4 * kArr <= 4976, "LDS of one wave");
+
 __device__ __forceinline__ uint32_t lds_off(const uint32_t *a) {
   typedef __attribute__((address_space(3))) const uint32_t lds_u32;
   return (uint32_t)(uintptr_t)(lds_u32 *)a;
 }
 
-// Five ds_mskor_rtn_b32 back to back, one wait: *a = (*a & ~clear) | set,
-// returning the old dword -- a 16-bit exchange inside a dword of two bucket
-// heads (no 16-bit LDS exchange exists).  The LDS serves one wave's
-// operations in order, so a later swap of the same head sees the earlier.
-__device__ __forceinline__ void mskor_rtn5(uint32_t (&old)[5], const uint32_t (&a)[5],
-                                           const uint32_t (&clr)[5], const uint32_t (&set)[5]) {
+// Five ds_wrxchg_rtn_b32 back to back, one wait: old = *(head base + a); *(...) = v.
+// The addresses are relative to the head array (kHeadOff, the instruction's
+// offset field); the LDS serves one wave's operations in order, so a later
+// exchange of the same head sees the earlier.
+__device__ __forceinline__ void xchg_rtn5(uint32_t (&old)[5], const uint32_t (&a)[5],
+                                          const uint32_t (&v)[5]) {
   asm volatile(
-      "ds_mskor_rtn_b32 %0, %5, %10, %15\n\t"
-      "ds_mskor_rtn_b32 %1, %6, %11, %16\n\t"
-      "ds_mskor_rtn_b32 %2, %7, %12, %17\n\t"
-      "ds_mskor_rtn_b32 %3, %8, %13, %18\n\t"
-      "ds_mskor_rtn_b32 %4, %9, %14, %19\n\t"
+      "ds_wrxchg_rtn_b32 %0, %5, %10 offset:368\n\t"
+      "ds_wrxchg_rtn_b32 %1, %6, %11 offset:368\n\t"
+      "ds_wrxchg_rtn_b32 %2, %7, %12 offset:368\n\t"
+      "ds_wrxchg_rtn_b32 %3, %8, %13 offset:368\n\t"
+      "ds_wrxchg_rtn_b32 %4, %9, %14 offset:368\n\t"
       "s_waitcnt lgkmcnt(0)"
       : "=&v"(old[0]), "=&v"(old[1]), "=&v"(old[2]), "=&v"(old[3]), "=&v"(old[4])
       : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]),
-        "v"(clr[0]), "v"(clr[1]), "v"(clr[2]), "v"(clr[3]), "v"(clr[4]),
-        "v"(set[0]), "v"(set[1]), "v"(set[2]), "v"(set[3]), "v"(set[4])
+        "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4])
       : "memory");
 }
 
@@ -296,12 +299,15 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   PROF_DECL;
   const bool search = LZ4R_VARIANT != 1 && LZ4R_VARIANT != 2;
   const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
-  constexpr int kHeadW = kH / 2;          // head dwords (u16 heads)
-  static_assert(kHeadW % 256 == 0, "head reset: 16-B stores");
-  constexpr uint32_t kEmpty2 = kNoLink | (kNoLink << 16);   // two empty heads
+  // 1024 u32 heads (4 KB) overlay the queue, the candidates and the front of
+  // ent and rec -- all dead until the heads are (ent and rec are written
+  // after the exchanges)
+  uint8_t *const sb = reinterpret_cast<uint8_t *>(&S);
+  static_assert(kH % 256 == 0 && kHeadOff == 368, "head reset: 16-B stores; asm offset");
 #pragma unroll
-  for (int i = 0; i < kHeadW / 256; ++i)  // empty heads (the previous block's queue)
-    reinterpret_cast<uint4 *>(S.head())[i * 64 + lane] = make_uint4(kEmpty2, kEmpty2, kEmpty2, kEmpty2);
+  for (int i = 0; i < kH / 256; ++i)      // empty heads (the previous block's data)
+    reinterpret_cast<uint4 *>(sb + kHeadOff)[i * 64 + lane] =
+        make_uint4(kNoLink, kNoLink, kNoLink, kNoLink);
   // Blocked layout: lane l owns the five positions p0 .. p0 + 4, p0 = 5 l
   // (lanes 60..63 own none of a 300-B block).  One 12-byte window per lane
   // gives all five 4-gram keys and preceding bytes; the five head swaps go
@@ -323,28 +329,26 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
                              __builtin_amdgcn_alignbyte(d1, d0, 2u),
                              __builtin_amdgcn_alignbyte(d1, d0, 3u), d1,
                              __builtin_amdgcn_alignbyte(d2, d1, 1u)};
-    uint32_t adr[5], clr[5], set[5], sh[5], hv[5];
+    uint32_t adr[5], set[5], hv[5];
+    // inactive positions exchange with a dword of rec[192..320), past the
+    // heads and zeroed after the exchanges (distinct addresses per lane)
+    const uint32_t dummy = (uint32_t)(kRecOff + 4 * (192 + 5 * (lane & 15)) - kHeadOff);
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int p = p0 + r;
+      const bool act = search && p < nk;
+      hv[r] = key[r] * 2654435761u;             // bucket = top 10 bits, tag = the next 5
+      adr[r] = act ? (hv[r] >> (32 - kHB)) << 2 : dummy + 4u * (uint32_t)r;
+      set[r] = (uint32_t)(4 * p);               // heads hold byte offsets 4 p
+    }
+    uint32_t old[5];
+    xchg_rtn5(old, adr, set);
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = p0 + r;
       S.rec[p] = 0u;                    // local(p) accumulator (branch-free: past n unused)
-      const bool act = search && p < nk;
-      hv[r] = key[r] * 2654435761u;             // bucket = top 10 bits, tag = the next 5
-      const uint32_t bk = hv[r] >> (32 - kHB);
-      sh[r] = (bk & 1u) << 4;
-      // inactive positions swap into their own entry dword, written after the
-      // swaps (distinct addresses: no serialised same-address atomics)
-      adr[r] = act ? lds_off(&S.head()[bk >> 1]) : lds_off(&S.ent[p]);
-      clr[r] = 0xFFFFu << sh[r];
-      set[r] = (uint32_t)(4 * p) << sh[r];               // heads hold byte offsets 4 p
-    }
-    uint32_t old[5];
-    mskor_rtn5(old, adr, clr, set);
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int p = p0 + r;
-      // the previous head as an 11-bit byte link (kNoLink: none)
-      const uint32_t link = __builtin_amdgcn_ubfe(old[r], sh[r], 11);
+      // the previous head: a byte link (kNoLink: none)
+      const uint32_t link = old[r];
       // blk[p - 1]; 256 for p = 0, which so differs from every byte and makes
       // every pair with j = 0 left-maximal
       uint32_t pb = r < 4 ? (d0 >> (8 * r)) & 255u : d1 & 255u;
