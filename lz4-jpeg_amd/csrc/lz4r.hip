@@ -288,14 +288,14 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   constexpr int base = kInOff;
 
   // ---- index: per-bucket chains of the 4-gram starts -----------------------
-  // Position p swaps itself into its bucket's u16 head (0xFFFF = empty) and
-  // keeps the previous head as its link.  The chains are in insertion order: rounds
-  // ascend, and lanes of one round that share a bucket are chained in the
-  // order the LDS served their swaps.  Entry:
-  //   link (9 bits, 511 = none) | preceding byte << 9 | 15-bit hash tag << 17.
+  // Position p exchanges itself (as the byte offset 4 p) into its bucket's
+  // u32 head (kNoLink = empty) and keeps the previous head as its link.  The
+  // chains are in insertion order: rounds ascend, and lanes of one round that
+  // share a bucket are chained in the order the LDS served their exchanges.
+  // Entry: link (11 bits) | 5-bit tag << 17 | preceding byte (9 bits) << 22.
   // Every unordered pair of a bucket is met once, by the later-inserted of
-  // the two walking its chain; walkers that continue are re-queued, so each
-  // pass over the queue is balanced over the lanes whatever the chain lengths.
+  // the two walking its chain; a lane keeps its walker until the chain ends,
+  // so each pass is balanced over the lanes whatever the chain lengths.
   PROF_DECL;
   const bool search = LZ4R_VARIANT != 1 && LZ4R_VARIANT != 2;
   const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
