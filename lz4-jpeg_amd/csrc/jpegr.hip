@@ -40,6 +40,8 @@ __constant__ double dAA88[8][8];
 __constant__ double dAA84[8][4];
 __constant__ int dLQ[64];
 __constant__ int dCQ[32];
+__constant__ double dLQr[64];   // RN(1 / T): the quantisation's fast path
+__constant__ double dCQr[32];
 __constant__ int dZZ8[64];
 __constant__ int dZZ4[32];
 __constant__ int dZZ8inv[64];   // zigzag index -> natural index
@@ -74,6 +76,33 @@ __device__ __forceinline__ void convert_pixel(uint32_t p, bool valid, int r,
     const int ci = tile * kCStride + r * 4 + (col >> 1);
     crl[ci] = (double)(crv - 128);
     cbl[ci] = (double)(cbv - 128);
+  }
+}
+
+// q = (int)(coef / T) (JPEG.c:626-627, IEEE division then truncation) for a
+// row of W coefficients.  r = RN(coef * RN(1/T)) and RN(coef / T) both lie
+// within ~1.5 ulp of coef / T (|r| < 2^12: ulp <= 2^-40), so their
+// truncations differ only when coef / T is that close to an integer; a lane
+// whose r is within 2^-30 of an integer (exact quotients and zeros included)
+// takes the IEEE division, the others truncate r.  The fallback is one
+// wave-uniform branch per row, so the division sequence runs only when some
+// lane of the wave needs it.
+template <int W>
+__device__ __forceinline__ void quantize_row(const double (&cf)[W], const int *T,
+                                             const double *rT, int (&q)[W]) {
+  bool slow = false;
+#pragma unroll
+  for (int v = 0; v < W; ++v) {
+    const double r = cf[v] * rT[v];
+    slow = slow || !(fabs(r - __builtin_rint(r)) > 0x1p-30);
+    q[v] = (int)r;
+  }
+  if (__builtin_amdgcn_ballot_w64(slow)) {
+#pragma unroll
+    for (int v = 0; v < W; ++v) {
+      const int qd = (int)(cf[v] / (double)T[v]);
+      q[v] = slow ? qd : q[v];
+    }
   }
 }
 
@@ -156,15 +185,14 @@ __global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
           s[v] = s[v] + tv * jpegr_tables::C8[y][v];             // *cos_y, +=
       }
     }
+    double cf[8];
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
-      const double coef = dAA88[u][v] * s[v];                    // JPEG.c:489
-      if (RAW) {
-        if (tile_ok) static_cast<double *>(out)[tile_g * 128 + u * 8 + v] = coef;
-      } else {
-        qy[v] = (int)(coef / (double)dLQ[u * 8 + v]);            // JPEG.c:626-627
-      }
+      cf[v] = dAA88[u][v] * s[v];                                // JPEG.c:489
+      if (RAW && tile_ok) static_cast<double *>(out)[tile_g * 128 + u * 8 + v] = cf[v];
     }
+    if (!RAW) quantize_row<8>(cf, &dLQ[u * 8], &dLQr[u * 8], qy);   // JPEG.c:626-627
+
   }
 
   // ---- phase 3: chroma DCTs row u (JPEG.c:1139-1140: width 4, height 8) ----
@@ -183,16 +211,13 @@ __global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
         for (int v = 0; v < 4; ++v) s[v] = s[v] + tv * jpegr_tables::C4[y][v];
       }
     }
+    double cf[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const double coef = dAA84[u][v] * s[v];
-      if (RAW) {
-        if (tile_ok)
-          static_cast<double *>(out)[tile_g * 128 + 64 + ch * 32 + u * 4 + v] = coef;
-      } else {
-        qc[ch][v] = (int)(coef / (double)dCQ[u * 4 + v]);
-      }
+      cf[v] = dAA84[u][v] * s[v];
+      if (RAW && tile_ok) static_cast<double *>(out)[tile_g * 128 + 64 + ch * 32 + u * 4 + v] = cf[v];
     }
+    if (!RAW) quantize_row<4>(cf, &dCQ[u * 4], &dCQr[u * 4], qc[ch]);
   }
 
   if (RAW) return;
@@ -401,6 +426,11 @@ hipError_t upload_tables() {
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dAA84), AA84, sizeof(AA84))) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dLQ), lq, sizeof(lq))) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dCQ), cq, sizeof(cq))) != hipSuccess) return e;
+  double lqr[64], cqr[32];
+  for (int i = 0; i < 64; ++i) lqr[i] = 1.0 / (double)lq[i];    // correctly rounded
+  for (int i = 0; i < 32; ++i) cqr[i] = 1.0 / (double)cq[i];
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dLQr), lqr, sizeof(lqr))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dCQr), cqr, sizeof(cqr))) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ8), z8, sizeof(z8))) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ4), z4, sizeof(z4))) != hipSuccess) return e;
   int i8[64], i4[32];
