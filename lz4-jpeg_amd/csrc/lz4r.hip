@@ -139,7 +139,7 @@ static_assert(kSlot % 16 == 0 && kSlot >= kBlkOutMax && kBlkOutMax / 16 <= 64,
 struct TileLds {
   alignas(16) uint8_t buf[kBufBytes];
   union {
-    uint32_t ent[kArr];   // per position: link | preceding byte << 9 | tag << 17
+    uint32_t ent[kArr];   // per position: link | tag << 17 | preceding byte << 22
     uint32_t nm[kArr];    // then: first matchable position >= x (dwords: no sub-dword LDS access)
   };
   uint32_t rec[kArr];     // local(p) accumulator; then dist | M<<9 | succ<<17
@@ -151,15 +151,9 @@ struct TileLds {
   __device__ __forceinline__ uint32_t *cand() { return reinterpret_cast<uint32_t *>(buf + kCandOff); }
 };
 
-constexpr int kEntOff = kBufBytes;              // byte offsets of ent and rec in TileLds
-constexpr int kRecOff = kBufBytes + 4 * kArr;
+constexpr int kRecOff = kBufBytes + 4 * kArr;   // byte offset of rec in TileLds
 static_assert(kHeadOff + 4 * kH <= kRecOff + 4 * 192, "u32 heads end before rec[192]");
 static_assert(kRecOff + 4 * kArr <= 4976, "LDS of one wave");
-
-__device__ __forceinline__ uint32_t lds_off(const uint32_t *a) {
-  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-  return (uint32_t)(uintptr_t)(lds_u32 *)a;
-}
 
 // Five ds_wrxchg_rtn_b32 back to back, one wait: old = *(head base + a); *(...) = v.
 // The addresses are relative to the head array (kHeadOff, the instruction's
