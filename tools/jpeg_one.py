@@ -1,4 +1,5 @@
-"""Run the JPEG encoder a few times on one 3840x2160 random image (for profilers)."""
+"""Run the JPEG encoder a few times on 3840x2160 random images (for profilers):
+jpeg_one.py [reps] [images per launch]."""
 import os
 import sys
 
@@ -9,9 +10,14 @@ from lz4jpeg import jpeg, synth  # noqa: E402
 
 w, h = 3840, 2160
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-img = torch.from_numpy(synth.rand_rgba(w, h, seed=1)).cuda()
-out = torch.empty(jpeg.coef_count(w, h), dtype=torch.int16, device="cuda")
+nimg = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+if nimg == 1:
+    img = torch.from_numpy(synth.rand_rgba(w, h, seed=1)).cuda()
+else:
+    img = torch.empty(4 * w * h * nimg, dtype=torch.uint8, device="cuda")
+    synth.rand_rgba_device(img, 0, w * h * nimg, seed=1)
+out = torch.empty(nimg * jpeg.coef_count(w, h), dtype=torch.int16, device="cuda")
 for _ in range(reps):
-    jpeg.encode_device(img, w, h, 1, out)
+    jpeg.encode_device(img, w, h, nimg, out)
 torch.cuda.synchronize()
 print("ok", flush=True)
