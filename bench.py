@@ -43,6 +43,10 @@ TRAFFIC_JSON = os.path.join(REPO, "profiles", "r02_traffic.json")
 # per-launch instruction counts of lz4_tiles + measured SIMD issue rates
 # (tools/issue.sh -> tools/issue_summary.py)
 ISSUE_JSON = os.path.join(REPO, "profiles", "r02_issue.json")
+# clock each kernel holds under its own load (DVFS give-back), from a
+# GRBM_GUI_ACTIVE PMC pass (tools/clock_pmc.sh -> tools/clock_summary.py)
+CLOCK_JSON = os.path.join(REPO, "profiles", "r02_clock.json")
+SPEC_CLOCK_GHZ = 2.4
 
 CFG4_BYTES = 64 << 30          # configs[3]
 CFG5_IMAGES = 1024             # configs[4]
@@ -61,6 +65,25 @@ def _profile_json(path):
     return old if os.path.exists(old) else path
 
 
+def held_clock(key):
+    """Median clock (GHz) the profiled kernel `key` held, or None."""
+    try:
+        return float(json.load(open(CLOCK_JSON))[key]["ghz_median"])
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
+
+
+def at_held_clock(achieved, peak_spec, key):
+    """The spec peak rescaled to the clock `key` holds under load, and the
+    fraction of that; {} when no clock profile is present."""
+    f = held_clock(key)
+    if not f:
+        return {}
+    p = peak_spec * f / SPEC_CLOCK_GHZ
+    return {"held_clock_ghz": f, "peak_at_held_clock": round(p, 2),
+            "frac_at_held_clock": round(achieved / p, 4)}
+
+
 def issue_roof(bytes_now, launch_ms):
     """The compressor's binding roof: wave-instruction issue.  Counts per
     launch from PMC (scaled to this input), rates from the micro-benchmark."""
@@ -75,8 +98,23 @@ def issue_roof(bytes_now, launch_ms):
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None
     sec = launch_ms / 1e3
+    # the micro-benchmark's rate was measured at the clock it held (valu_rate's
+    # v_add body); per cycle, the kernel's own clock sets its peak
+    clk = {}
+    fk, fb = held_clock("lz4:lz4_tiles"), held_clock("valu:void body<0>")
+    fm = held_clock("valu:void body<3>")               # the 4 VALU + 4 SALU body
+    if fk and fb:
+        pk = peak_valu * fk / fb
+        clk = {"held_clock_ghz": fk, "bench_clock_ghz": fb,
+               "peak_at_held_clock": round(pk / 1e9, 1),
+               "frac_at_held_clock": round(valu / sec / pk, 4)}
+        if fm:
+            pm = peak_mix * fk / fm
+            clk["mixed_stream_peak_at_held_clock"] = round(pm / 1e9, 1)
+            clk["valu_salu_frac_at_held_clock"] = round((valu + salu) / sec / pm, 4)
     return {
-        "bound": "issue (VALU wave-instructions)", "unit": "Gwinstr/s",
+        **clk,
+        "bound": "issue (VALU + SALU wave-instructions)", "unit": "Gwinstr/s",
         "achieved": round(valu / sec / 1e9, 1), "peak": round(peak_valu / 1e9, 1),
         "frac": round(valu / sec / peak_valu, 4),
         "valu_salu_gwinstr_s": round((valu + salu) / sec / 1e9, 1),
@@ -88,9 +126,11 @@ def issue_roof(bytes_now, launch_ms):
         "note": "achieved = PMC SQ_INSTS_VALU per launch (" +
                 os.path.basename(_profile_json(ISSUE_JSON)) + ", scaled to this input) / "
                 "lz4_tiles time; peak = the chip's measured v_add/xor/and/or rate at 8 waves "
-                "per SIMD (tools/valu_rate.hip).  VALU + SALU together exceed the rate of an "
-                "interleaved 4 VALU + 4 SALU stream (mixed_stream_peak: SALU of other waves "
-                "issues beside VALU), so the VALU rate is the binding issue roof",
+                "per SIMD (tools/valu_rate.hip).  At the clocks each holds under load "
+                "(" + os.path.basename(CLOCK_JSON) + ": the micro-benchmark bodies run slower "
+                "than lz4_tiles) the kernel's VALU + SALU issue runs at "
+                "valu_salu_frac_at_held_clock of an interleaved 4 VALU + 4 SALU stream: "
+                "VALU and SALU instructions together are the binding issue roof",
     }
 
 
@@ -519,8 +559,12 @@ def run_jpeg(ctx, total_images, scaling):
                 "achieved": round(tiles * 13312 / (kern_ms / 1e3) / 1e12, 2),
                 "peak": FP64_VALU_PEAK_TOPS,
                 "frac": round(tiles * 13312 / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
+                **at_held_clock(tiles * 13312 / (kern_ms / 1e3) / 1e12, FP64_VALU_PEAK_TOPS,
+                                "jpeg:void jpeg_strip_kernel<false>"),
                 "note": "13312 non-fused fp64 mul/add per tile in reference order "
-                        "(8704 luma + 2x2304 chroma); peak = 78.6 TF fp64 vector spec / 2",
+                        "(8704 luma + 2x2304 chroma); peak = 78.6 TF fp64 vector spec / 2 at "
+                        "2.4 GHz; peak_at_held_clock = the same per cycle at the clock the "
+                        "kernel holds under its own load (" + os.path.basename(CLOCK_JSON) + ")",
             },
             "note": "8 B/pixel algorithmic (4 B RGBA read + 4 B int16 written); traffic "
                     "from PMC FETCH_SIZE x2 + WRITE_SIZE",
@@ -556,6 +600,8 @@ def run_jpeg(ctx, total_images, scaling):
                 "bound": "valu_fp64", "unit": "Tops/s", "peak": FP64_VALU_PEAK_TOPS,
                 "achieved": round(btiles * 13312 / (bms / 1e3) / 1e12, 2),
                 "frac": round(btiles * 13312 / (bms / 1e3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
+                **at_held_clock(btiles * 13312 / (bms / 1e3) / 1e12, FP64_VALU_PEAK_TOPS,
+                                "jpeg:void jpeg_strip_kernel<false>"),
                 "hbm_frac": round(8 * px * NB / (bms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
             "note": "images 0..127 of the continuous rand() stream: config 5's per-GPU share "
                     "at 8 GPUs, on one GPU",

@@ -536,14 +536,33 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   };
   const int n4 = 4 * n;
   int c4 = F0, it = 0;
+  // lane k of seqv: the record word whose successor field (bits 17..) is 4 c_k
+  // (for k = 0 a made-up word, F0 << 17).  Per sequence: the word goes to lane
+  // it (m0, which is also the counter: lane select = it mod 64; past 64
+  // sequences lanes are overwritten and the walk is redone below), the next
+  // word is read at the successor's byte offset, and the loop goes on while
+  // word < 4 n << 17 -- the same test as 4 c < 4 n, with no shift.  Two SALU
+  // and three VALU per sequence (a C++ loop took four SALU: m0 set from a
+  // counter, the counter, the shift, the compare).
   uint32_t seqv = 0;
-  while (c4 < n4) {
-    // lane select = it mod 64: past 64 sequences lanes are overwritten and
-    // the walk is redone below
-    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
-                 : "+v"(seqv) : "s"(c4), "s"(it));   // m0: the lane select (one SGPR read per VOP3)
-    ++it;
-    c4 = succ4(c4);
+  if (c4 < n4) {
+    static_assert(kRecOff < 65536, "ds_read offset field");
+    uint32_t w = (uint32_t)F0 << 17, va = (uint32_t)F0, vt;
+    asm volatile(
+        "s_mov_b32 m0, 0\n"
+        "1:\n\t"
+        "v_writelane_b32 %0, %1, m0\n\t"
+        "ds_read_b32 %3, %2 offset:%c6\n\t"
+        "s_add_u32 m0, m0, 1\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_readfirstlane_b32 %1, %3\n\t"
+        "v_lshrrev_b32 %2, 17, %3\n\t"
+        "s_cmp_lt_u32 %1, %5\n\t"
+        "s_cbranch_scc1 1b\n\t"
+        "s_mov_b32 %4, m0"
+        : "+v"(seqv), "+s"(w), "+v"(va), "=&v"(vt), "=s"(it)
+        : "s"((uint32_t)n4 << 17), "i"(kRecOff)
+        : "scc", "memory");   // (m0 is reserved: no other use in this kernel)
   }
   // Past 64 sequences (only with truncated matches) the walk is redone into S.seq.
   const bool slow = it > 64;
@@ -573,7 +592,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     const int kk = s0 + lane;
     uint32_t cq;
     if (!slow) {
-      cq = kk < it ? seqv >> 2 : (uint32_t)n;                     // (kk < it only in round 0)
+      cq = kk < it ? seqv >> 19 : (uint32_t)n;                    // (kk < it only in round 0)
     } else {
       cq = kk < Sv_slow ? S.seq()[kk] : (uint32_t)n;
     }
