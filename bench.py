@@ -424,7 +424,7 @@ def run_lz4(ctx, n_total, scaling):
         "value": round(n_total / (bdt / args.steps) / 1e9, 3), "unit": "GB/s",
         "call_ms": round(bdt / args.steps * 1e3, 4), "roundtrip_ok": bare_ok,
         "note": "whole synchronous call: on-device block-boundary discovery (lz4_bare_*), "
-                "lz4_decode_blocks, two host read-backs"}
+                "lz4_decode_blocks, one host read-back"}
     log(f"lz4 bare-stream decode: {bdt / args.steps * 1e3:.3f} ms/call, "
         f"{lz4_dec['bare_stream']['value']} GB/s, ok={bare_ok}")
 

@@ -48,6 +48,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/lz4r.h"
 
 namespace {
@@ -332,13 +334,21 @@ __device__ __forceinline__ int decode_block(const BytesT &p, int len, bool last,
   }
 }
 
+// nb_dev (bare streams): the block count is read on the device, the grid is
+// sized for an upper bound, and nothing is decoded unless *gate is 0
 __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
     const uint8_t *__restrict__ in, size_t in_len, const uint64_t *__restrict__ boff,
     size_t nb, uint8_t *__restrict__ out, size_t out_cap,
-    unsigned long long *__restrict__ result) {
+    unsigned long long *__restrict__ result, const unsigned long long *__restrict__ nb_dev,
+    const unsigned long long *__restrict__ gate) {
   __shared__ DecLds S;
   const int lane = threadIdx.x;
   const size_t b0 = (size_t)blockIdx.x * kLanes;
+  if (nb_dev) {
+    if (*gate != 0) return;
+    nb = (size_t)*nb_dev;
+  }
+  if (b0 >= nb) return;
   const int nl = (int)(nb - b0 < (size_t)kLanes ? nb - b0 : kLanes);   // blocks here
   const size_t b = b0 + lane;
 
@@ -521,14 +531,15 @@ __device__ __forceinline__ int bare_block_len(const uint8_t *in, size_t in_len, 
 template <bool kExact, bool kWrite>
 __device__ __forceinline__ uint64_t bare_walk_chunk(const uint8_t *in, size_t in_len, size_t c,
                                                     uint64_t x, uint32_t &cnt,
-                                                    uint64_t *boff, uint64_t base) {
+                                                    uint64_t *boff, uint64_t base,
+                                                    uint64_t boff_cap = 0) {
   cnt = 0;
   if (x == kNone || x == kBad) return kBad;
   const uint64_t lim = 1 + (c + 1) * (uint64_t)kChunkB;
   while (x < lim && x < in_len) {
     const int L = bare_block_len<kExact>(in, in_len, x);
     if (L == 0) return kBad;
-    if (kWrite) boff[base + cnt] = x - 1;
+    if (kWrite && base + cnt < boff_cap) boff[base + cnt] = x - 1;
     ++cnt;
     x += (uint64_t)L;
   }
@@ -691,7 +702,8 @@ __global__ __launch_bounds__(64) void lz4_bare_offsets(const uint8_t *__restrict
                                                        const uint64_t *__restrict__ cand,
                                                        const uint32_t *__restrict__ cnt,
                                                        const unsigned long long *__restrict__ gbase,
-                                                       uint64_t *__restrict__ boff) {
+                                                       uint64_t *__restrict__ boff,
+                                                       uint64_t boff_cap) {
   const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
   const uint32_t v = c < nchunks ? cnt[c] : 0u;
   uint32_t x = v;
@@ -703,7 +715,22 @@ __global__ __launch_bounds__(64) void lz4_bare_offsets(const uint8_t *__restrict
   if (c >= nchunks) return;
   const uint64_t base = gbase[blockIdx.x] + x - v;
   uint32_t n = 0;
-  bare_walk_chunk<kExact, true>(in, in_len, c, cand[c], n, boff, base);
+  bare_walk_chunk<kExact, true>(in, in_len, c, cand[c], n, boff, base, boff_cap);
+}
+
+// One thread: the chain's verdict before any block is decoded -- 0 = go,
+// 1 = corrupt (a broken chain, no block, or a frame byte that is not the
+// block count mod 256), 2 = more blocks than the output can hold (and so
+// than the offsets array) -- and the decoder's result slots reset.
+__global__ void lz4_bare_gate(const uint8_t *__restrict__ in, unsigned long long *small,
+                              uint64_t nb_cap) {
+  const unsigned long long nb = small[0], st = small[1];
+  unsigned long long g = 0;
+  if (st != 0 || nb == 0 || (uint8_t)(nb & 0xFF) != in[0]) g = 1;
+  else if (nb > nb_cap) g = 2;
+  small[2] = 0ull;
+  small[3] = ~0ull;
+  small[4] = g;
 }
 
 __global__ void lz4_decode_init(unsigned long long *result) {
@@ -727,23 +754,26 @@ extern "C" int lz4r_decompress_device(const void *d_in, size_t in_len, const voi
                      static_cast<const uint8_t *>(d_in), in_len,
                      static_cast<const uint64_t *>(d_block_offsets), nb,
                      static_cast<uint8_t *>(d_out), out_cap,
-                     static_cast<unsigned long long *>(d_result));
+                     static_cast<unsigned long long *>(d_result), nullptr, nullptr);
   return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
 }
 
 namespace {
 
 // one pass of the bare-stream decode in mode kExact; returns LZ4R_OK, or
-// LZ4R_ERR_CORRUPT when the chain or a block does not hold together
+// LZ4R_ERR_CORRUPT when the chain or a block does not hold together.  With
+// boff given (nb_cap of them: the most blocks out_cap can hold), one host
+// read-back: the block count stays on the device, the decoder's grid is sized
+// for nb_cap and lz4_bare_gate decides on the device whether anything is
+// decoded.  Without (an out_cap far above the stream's possible output), the
+// block count is read back first and sizes both.
 template <bool kExact>
 int bare_pass(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap, size_t nchunks,
               uint64_t *cand, uint32_t *cnt, uint64_t *exitp, unsigned long long *gsum,
-              unsigned long long *gbase, unsigned long long *small, size_t *out_len,
-              hipStream_t s) {
+              unsigned long long *gbase, unsigned long long *small, unsigned int *nmis,
+              unsigned int *mis, uint64_t *boff, size_t nb_cap, size_t *out_len, hipStream_t s) {
   const unsigned ng = (unsigned)((nchunks + 63) / 64);
-  unsigned long long *d_nb = small, *d_status = small + 1, *d_res = small + 2;
-  unsigned int *nmis = reinterpret_cast<unsigned int *>(small + 4);
-  unsigned int *mis = reinterpret_cast<unsigned int *>(small + 5);
+  unsigned long long *d_nb = small, *d_status = small + 1, *d_res = small + 2, *d_gate = small + 4;
   hipLaunchKernelGGL(lz4_bare_walk<kExact>, dim3(ng), dim3(64), 0, s, in, in_len, nchunks, cand,
                      cnt, exitp, gsum);
   if (hipMemsetAsync(nmis, 0, sizeof(unsigned int), s) != hipSuccess) return LZ4R_ERR_HIP;
@@ -752,31 +782,39 @@ int bare_pass(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap, si
   hipLaunchKernelGGL(lz4_bare_fix<kExact>, dim3(1), dim3(64), 0, s, in, in_len, nchunks, cand, cnt,
                      exitp, gsum, nmis, mis, d_status);
   hipLaunchKernelGGL(lz4_bare_scan, dim3(1), dim3(1024), 0, s, gsum, (size_t)ng, gbase, d_nb);
-  unsigned long long h[2] = {0, 0};
-  uint8_t frame = 0;
-  if (hipMemcpyAsync(h, small, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(&frame, in, 1, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return LZ4R_ERR_HIP;
-  const size_t nb = (size_t)h[0];
-  if (h[1] != 0 || nb == 0 || (uint8_t)(nb & 0xFF) != frame) return LZ4R_ERR_CORRUPT;
-  uint64_t *boff = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void **>(&boff), nb * sizeof(uint64_t), s) != hipSuccess)
-    return LZ4R_ERR_NOMEM;
+  uint64_t *own = nullptr;
+  if (!boff) {
+    // no useful bound from out_cap: read the block count first
+    unsigned long long h2[2] = {0, 0};
+    if (hipMemcpyAsync(h2, small, sizeof(h2), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return LZ4R_ERR_HIP;
+    if (h2[1] != 0 || h2[0] == 0) return LZ4R_ERR_CORRUPT;
+    nb_cap = (size_t)h2[0];
+    if (hipMallocAsync(reinterpret_cast<void **>(&own), nb_cap * sizeof(uint64_t), s) !=
+        hipSuccess)
+      return LZ4R_ERR_NOMEM;
+    boff = own;
+  }
   hipLaunchKernelGGL(lz4_bare_offsets<kExact>, dim3(ng), dim3(64), 0, s, in, in_len, nchunks, cand,
-                     cnt, gbase, boff);
-  hipLaunchKernelGGL(lz4_decode_init, dim3(1), dim3(1), 0, s, d_res);
-  hipLaunchKernelGGL(lz4_decode_blocks, dim3((unsigned)((nb + kLanes - 1) / kLanes)), dim3(kLanes),
-                     0, s, in, in_len, static_cast<const uint64_t *>(boff), nb, out,
-                     out_cap, d_res);
-  (void)hipFreeAsync(boff, s);
-  unsigned long long r[2] = {0, 0};
-  if (hipMemcpyAsync(r, d_res, sizeof(r), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                     cnt, gbase, boff, (uint64_t)nb_cap);
+  hipLaunchKernelGGL(lz4_bare_gate, dim3(1), dim3(1), 0, s, in, small, (uint64_t)nb_cap);
+  hipLaunchKernelGGL(lz4_decode_blocks, dim3((unsigned)((nb_cap + kLanes - 1) / kLanes)),
+                     dim3(kLanes), 0, s, in, in_len, static_cast<const uint64_t *>(boff), nb_cap,
+                     out, out_cap, d_res, d_nb, d_gate);
+  if (own) (void)hipFreeAsync(own, s);
+  unsigned long long h[5] = {0, 0, 0, 0, 0};          // nb, status, result[2], gate
+  if (hipMemcpyAsync(h, small, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return LZ4R_ERR_HIP;
-  if (r[1] != ~0ull) return LZ4R_ERR_CORRUPT;
-  *out_len = (size_t)r[0];
-  return r[0] > out_cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
+  if (h[4] == 1) return LZ4R_ERR_CORRUPT;
+  if (h[4] == 2) {                                    // at least this much output
+    *out_len = (size_t)(h[0] - 1) * kBlk + 1;
+    return LZ4R_ERR_CAPACITY;
+  }
+  if (h[3] != ~0ull) return LZ4R_ERR_CORRUPT;
+  *out_len = (size_t)h[2];
+  return h[2] > out_cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
 }
 
 }  // namespace
@@ -791,28 +829,41 @@ extern "C" int lz4r_decompress_stream_device(const void *d_in, size_t in_len, vo
   uint8_t *out = static_cast<uint8_t *>(d_out);
   const size_t nchunks = (in_len - 1 + kChunkB - 1) / kChunkB;
   const size_t ng = (nchunks + 63) / 64;
-  // scratch: cand, exit (u64), cnt (u32) per chunk; gsum, gbase per 64 chunks; nb, status,
-  // result[2], the inconsistent-chunk count and list (kMisCap u32)
-  const size_t bytes = nchunks * 20 + ng * 16 + 5 * 8 + 4 * (size_t)kMisCap + 64;
+  // blocks the output can hold (every block but the last decodes to 300
+  // bytes): the size of the offsets array and of the decoder's grid -- when
+  // that is tighter than what the stream can hold (a block is >= 8 bytes);
+  // else (an oversized out_cap) the count is read back first (nb_cap 0)
+  const size_t nb_out = out_cap / kBlk + 1, nb_in = (in_len - 1) / 8 + 1;
+  const size_t nb_cap = nb_out <= nb_in ? nb_out : 0;
+  // scratch: cand, exit (u64) per chunk; gsum, gbase per 64 chunks; 8 u64 of
+  // nb, status, result[2], gate, the inconsistent-chunk count; the list
+  // (kMisCap u32); cnt (u32) per chunk; the block offsets (nb_cap u64)
+  const size_t o_gsum = 16 * nchunks, o_small = o_gsum + 16 * ng, o_mis = o_small + 64;
+  const size_t o_cnt = o_mis + 4 * (size_t)kMisCap;
+  const size_t o_boff = (o_cnt + 4 * nchunks + 7) & ~(size_t)7;
+  const size_t bytes = o_boff + 8 * nb_cap;
   uint8_t *scr = nullptr;
   if (hipMallocAsync(reinterpret_cast<void **>(&scr), bytes, s) != hipSuccess) return LZ4R_ERR_NOMEM;
   uint64_t *cand = reinterpret_cast<uint64_t *>(scr);
   uint64_t *exitp = cand + nchunks;
-  unsigned long long *gsum = reinterpret_cast<unsigned long long *>(exitp + nchunks);
+  unsigned long long *gsum = reinterpret_cast<unsigned long long *>(scr + o_gsum);
   unsigned long long *gbase = gsum + ng;
-  unsigned long long *small = gbase + ng;
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(small + 5 + kMisCap / 2);
+  unsigned long long *small = reinterpret_cast<unsigned long long *>(scr + o_small);
+  unsigned int *nmis = reinterpret_cast<unsigned int *>(small + 5);
+  unsigned int *mis = reinterpret_cast<unsigned int *>(scr + o_mis);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(scr + o_cnt);
+  uint64_t *boff = reinterpret_cast<uint64_t *>(scr + o_boff);
   hipLaunchKernelGGL(lz4_bare_cand, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, in,
                      in_len, nchunks, cand);
   // fast mode (block length = its size field); the exact mode parses every
   // block and is needed only for streams with truncated matches
   int rc = bare_pass<false>(in, in_len, out, out_cap, nchunks, cand, cnt, exitp, gsum, gbase,
-                            small, out_len, s);
+                            small, nmis, mis, nb_cap ? boff : nullptr, nb_cap, out_len, s);
   if (rc == LZ4R_ERR_CORRUPT) {
     hipLaunchKernelGGL(lz4_bare_cand, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, in,
                        in_len, nchunks, cand);
     rc = bare_pass<true>(in, in_len, out, out_cap, nchunks, cand, cnt, exitp, gsum, gbase, small,
-                         out_len, s);
+                         nmis, mis, nb_cap ? boff : nullptr, nb_cap, out_len, s);
   }
   (void)hipFreeAsync(scr, s);
   if (hipStreamSynchronize(s) != hipSuccess) return LZ4R_ERR_HIP;

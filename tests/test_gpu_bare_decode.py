@@ -100,6 +100,26 @@ def test_bare_many_blocks_and_tight_capacity(comp):
     assert ei.value.code == -3
 
 
+def test_bare_output_capacity_paths(comp):
+    """An output buffer that cannot hold the stream's block count is a
+    capacity error before anything is decoded (the device-side gate); one far
+    larger than the stream could decode to takes the path that reads the
+    block count back first, and decodes the same bytes."""
+    import torch
+    from lz4jpeg import lz4
+    data = golden_inputs.lz4_input("file:Metamorphosis.txt")
+    b = np.frombuffer(data, dtype=np.uint8)
+    d_in = torch.from_numpy(b.copy()).cuda()
+    d_stream, length = comp.compress_device(d_in)
+    for cap in (1, 299, 301, 3000):
+        with pytest.raises(lz4.Lz4Error) as ei:
+            lz4.decompress_stream_device(d_stream, length, cap)
+        assert ei.value.code == -3, cap
+    big = 300 * (length // 8 + 8)
+    d_out, got = lz4.decompress_stream_device(d_stream, length, big)
+    assert got == b.size and torch.equal(d_out[:b.size], d_in)
+
+
 def test_bare_structural_corruption_reported(gpu, oracle):
     from lz4jpeg import lz4
     data = golden_inputs.lz4_input("metamorphosis_spaces")[:50_000]
