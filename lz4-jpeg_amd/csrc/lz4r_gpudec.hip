@@ -9,10 +9,10 @@
 // split in parallel (the u16 size field over-counts the truncated-length
 // sequences, LZ4.c:569-575).
 //
-// Mapping: one LANE per block, 64 consecutive blocks per wave (a wave per
+// Mapping: one LANE per block, 32 consecutive blocks per wave (a wave per
 // block would issue every serial parsing step as a full wave instruction).
 // The walk is latency- and issue-bound, so the kernel keeps LDS small for
-// occupancy (19.5 KB of LDS per wave: the 64 output slots; 8 waves/CU) and
+// occupancy (9.6 KB of LDS per wave: the 32 output slots; 16 waves/CU) and
 // keeps instruction counts low:
 //   - the lane reads its encoded bytes with single unaligned 8/16-byte
 //     global loads (L1/L2 absorb the re-reads of the wave's ~20 KB range),
@@ -29,7 +29,7 @@
 //     runs in unaligned mode) whose bytes past the wanted ones fall beyond
 //     the lane's write frontier; within 16 bytes of the slot end they are
 //     exact-size (b64/b32/b16/b8 pieces), so no lane touches a neighbour;
-//   - the wave's 64 x 300 = 19200 contiguous bytes leave as 16-B stores.
+//   - the wave's 32 x 300 = 9600 contiguous bytes leave as 16-B stores.
 // Measured alternatives that lost (1 GiB text, MI355X): one wave per block
 // (15.5 ms), nested copy loops with byte stores (3.4 ms), staging the wave's
 // input in LDS (halves occupancy: 2x slower), output slots in global memory
@@ -56,7 +56,12 @@ namespace {
 
 constexpr int kBlk = LZ4R_BLOCK;
 constexpr int kInMax = LZ4R_BLOCK_BOUND;   // bytes of one encoded block (bound)
-constexpr int kLanes = 64;                 // blocks per workgroup (one wave)
+constexpr int kLanes = 64;                 // threads per workgroup (one wave)
+// blocks per wave (lanes 0 .. kBPW-1 decode; all 64 lanes store the wave's
+// output): 32 x 300 B of LDS lets 16 waves share a CU where 64 blocks per wave
+// allowed 8 -- the walk is latency-bound, so more, narrower waves win (1 GiB:
+// 64 -> 1.68 ms, 48 -> 1.68, 40 -> 1.68, 32 -> 1.59, 24 -> 1.61, 16 -> 1.95)
+constexpr int kBPW = 32;
 constexpr int kDepth = 10;                 // choice points per lane (<= 9 needed)
 constexpr int kMaxSteps = 1 << 16;         // header budget: a hostile stream cannot spin a lane
 constexpr int kPfN = 4;                    // L2 lines touched ahead of the walk
@@ -67,7 +72,7 @@ typedef uint32_t u32u __attribute__((aligned(1)));
 typedef uint16_t u16u __attribute__((aligned(1)));
 
 struct DecLds {
-  alignas(16) uint8_t out[kLanes * kBlk + 32];   // lane l's block at out[300 l] (+ slack)
+  alignas(16) uint8_t out[kBPW * kBlk + 32];     // lane l's block at out[300 l] (+ slack)
   uint32_t qlen[kLanes];                         // decoded bytes per block (0 = failed)
 };
 
@@ -343,13 +348,13 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
     const unsigned long long *__restrict__ gate) {
   __shared__ DecLds S;
   const int lane = threadIdx.x;
-  const size_t b0 = (size_t)blockIdx.x * kLanes;
+  const size_t b0 = (size_t)blockIdx.x * kBPW;
   if (nb_dev) {
     if (*gate != 0) return;
     nb = (size_t)*nb_dev;
   }
   if (b0 >= nb) return;
-  const int nl = (int)(nb - b0 < (size_t)kLanes ? nb - b0 : kLanes);   // blocks here
+  const int nl = (int)(nb - b0 < (size_t)kBPW ? nb - b0 : kBPW);       // blocks here
   const size_t b = b0 + lane;
 
   int q = 0;                                         // decoded bytes (0 = failed / absent)
@@ -744,12 +749,12 @@ extern "C" int lz4r_decompress_device(const void *d_in, size_t in_len, const voi
                                       size_t nb, void *d_out, size_t out_cap, void *d_result,
                                       void *stream) {
   if (!d_in || !d_block_offsets || !d_out || !d_result || nb == 0 || in_len < 4 ||
-      nb > 0x7fffffffULL * kLanes)
+      nb > 0x7fffffffULL * kBPW)
     return LZ4R_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(lz4_decode_init, dim3(1), dim3(1), 0, s,
                      static_cast<unsigned long long *>(d_result));
-  const unsigned grid = (unsigned)((nb + kLanes - 1) / kLanes);
+  const unsigned grid = (unsigned)((nb + kBPW - 1) / kBPW);
   hipLaunchKernelGGL(lz4_decode_blocks, dim3(grid), dim3(kLanes), 0, s,
                      static_cast<const uint8_t *>(d_in), in_len,
                      static_cast<const uint64_t *>(d_block_offsets), nb,
@@ -799,7 +804,7 @@ int bare_pass(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap, si
   hipLaunchKernelGGL(lz4_bare_offsets<kExact>, dim3(ng), dim3(64), 0, s, in, in_len, nchunks, cand,
                      cnt, gbase, boff, (uint64_t)nb_cap);
   hipLaunchKernelGGL(lz4_bare_gate, dim3(1), dim3(1), 0, s, in, small, (uint64_t)nb_cap);
-  hipLaunchKernelGGL(lz4_decode_blocks, dim3((unsigned)((nb_cap + kLanes - 1) / kLanes)),
+  hipLaunchKernelGGL(lz4_decode_blocks, dim3((unsigned)((nb_cap + kBPW - 1) / kBPW)),
                      dim3(kLanes), 0, s, in, in_len, static_cast<const uint64_t *>(boff), nb_cap,
                      out, out_cap, d_res, d_nb, d_gate);
   if (own) (void)hipFreeAsync(own, s);
