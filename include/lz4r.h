@@ -155,7 +155,12 @@ int lz4r_decompress_device(const void *d_in, size_t in_len, const void *d_block_
  * block.  d_in / d_out are device pointers; synchronises `stream`;
  * *out_len = decoded length.  LZ4R_ERR_CORRUPT when the blocks do not chain
  * from the frame byte to the end of the stream or a block does not decode;
- * LZ4R_ERR_CAPACITY (with *out_len = need) when out_cap is too small. */
+ * LZ4R_ERR_CAPACITY (with *out_len = need, or a lower bound on it when the
+ * stream has more blocks than out_cap can hold) when out_cap is too small.
+ * One host read-back per pass when out_cap / 300 + 1 <= (in_len - 1) / 8 + 1
+ * (the output bounds the block count); a larger out_cap reads the block
+ * count back first.  Device scratch: ~20 B per 4 KiB of stream + 8 B per
+ * block out_cap can hold (stream-ordered allocation, freed on return). */
 int lz4r_decompress_stream_device(const void *d_in, size_t in_len, void *d_out,
                                   size_t out_cap, size_t *out_len, void *stream);
 
