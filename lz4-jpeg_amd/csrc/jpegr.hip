@@ -274,27 +274,41 @@ __global__ __launch_bounds__(kThreads) void jpeg_recon_kernel(
   const int t = threadIdx.x;
 
   // ---- phase 1: coefficients -> dequantised, alpha-scaled doubles ---------
+  // Thread t takes the 8 coefficients z0 .. z0 + 7 (z0 = 8 (t mod 16)) of
+  // tiles t / 16 and 16 + t / 16, so its natural indices, quantiser steps and
+  // alpha products are looked up once for both tiles.
   {
     const int16_t *src = coef + ((size_t)img * tiles_y * tiles_x + tile0) * 128;
+    const int z0 = (t & 15) * 8;
+    const bool luma = z0 < 64;
+    double *const dst = luma ? yac : (z0 < 96 ? crac : cbac);
+    const int stride = luma ? kYStride : kCStride;
+    int nat[8];
+    double qs[8], aa[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (luma) {
+        const int n8 = dZZ8inv[z0 + j];
+        nat[j] = n8;
+        qs[j] = (double)dLQ[n8];
+        aa[j] = dAA88[n8 >> 3][n8 & 7];
+      } else {
+        const int n4 = dZZ4inv[(z0 + j - 64) & 31];
+        nat[j] = n4;
+        qs[j] = (double)dCQ[n4];
+        aa[j] = dAA84[n4 >> 2][n4 & 3];
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const int e0 = (k * kThreads + t) * 8;          // 8 int16 per thread per step
-      if (e0 < ntiles * 128) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(src + e0);
+      const int tile = k * 16 + (t >> 4);
+      if (tile < ntiles) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(src + tile * 128 + z0);
         const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int e = e0 + j, tile = e >> 7, z = e & 127;
           const double q = (double)(int16_t)(wv[j >> 1] >> (16 * (j & 1)));
-          if (z < 64) {
-            const int nat = dZZ8inv[z];
-            yac[tile * kYStride + nat] = dAA88[nat >> 3][nat & 7] * (q * (double)dLQ[nat]);
-          } else {
-            const int zc = (z - 64) & 31, nat = dZZ4inv[zc];
-            const double a = dAA84[nat >> 2][nat & 3] * (q * (double)dCQ[nat]);
-            if (z < 96) crac[tile * kCStride + nat] = a;
-            else cbac[tile * kCStride + nat] = a;
-          }
+          dst[tile * stride + nat[j]] = aa[j] * (q * qs[j]);   // JPEG.c:631-638
         }
       }
     }
