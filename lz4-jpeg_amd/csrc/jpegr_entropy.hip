@@ -374,12 +374,14 @@ constexpr size_t kWorkBytesPerLane = 2 * kFullCap /*sym*/ + 2 * kFullCap /*hash*
 
 // ---- decode ------------------------------------------------------------------
 
-constexpr int kDecCap = 32;                // codes held in LDS (more: regenerated per symbol)
-
-template <int N>
+// Codes held in LDS per stream (more: regenerated per symbol), sized like
+// the encoder's working set (luma 24, chroma 12): 20 / 10 KB per wave, so a
+// 4K image's 2,025 luma and 4,050 chroma waves each run as ONE round of the
+// chip's wave slots (with 32 codes: 24 / 20 KB, two rounds each)
+template <int N, int Cap>
 struct DecLds {
-  uint32_t lc[kDecCap][kLanes];            // left-aligned codes, increasing
-  uint32_t vl[kDecCap][kLanes];            // value | len << 16
+  uint32_t lc[Cap][kLanes];                // left-aligned codes, increasing
+  uint32_t vl[Cap][kLanes];                // value | len << 16
   alignas(16) int16_t out[kLanes][N];      // the lane's decoded ints (leave as 16-B stores)
 };
 
@@ -465,9 +467,9 @@ __device__ bool decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
   return true;
 }
 
-// Streams with more codes than the LDS table holds (> 64: only luma streams
-// of nearly all-distinct ints): the codes are regenerated from the table for
-// every symbol and searched linearly -- slow, rare, no storage.
+// Streams with more codes than the LDS table holds (> 24 luma / 12 chroma:
+// the encoder's deferred streams): the codes are regenerated from the table
+// for every symbol and searched linearly -- slow, rare, no storage.
 __device__ bool decode_stream_slow(const uint8_t *__restrict__ bits, uint32_t m,
                                    const uint32_t *__restrict__ table, int16_t *__restrict__ out,
                                    int n) {
@@ -514,7 +516,8 @@ __global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
     const uint8_t *__restrict__ bits, const uint32_t *__restrict__ meta,
     const uint32_t *__restrict__ table, size_t ntiles, int16_t *__restrict__ coef,
     uint32_t *__restrict__ status) {
-  __shared__ DecLds<kLuma ? 64 : 32> S;
+  constexpr int Cap = kLuma ? kFastCap : kChromaCap;
+  __shared__ DecLds<kLuma ? 64 : 32, Cap> S;
   const int lane = threadIdx.x;
   const int c = kLuma ? 0 : 1 + (int)(blockIdx.x & 1);
   const size_t tile = (size_t)(kLuma ? blockIdx.x : blockIdx.x >> 1) * kLanes + lane;
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
   // a foreign or corrupted meta word must not index past the stream's slot:
   // its bits (bits_cap bits) and its table (2 n entries: RLE of n ints)
   const bool sane = (int)(m & 0xFFFF) <= bits_cap(c) && U <= 2 * n;
-  const bool ok = sane && (U <= kDecCap
+  const bool ok = sane && (U <= Cap
                                ? decode_stream(b, m, t, Col<uint32_t>{&S.lc[0][lane], kLanes},
                                                Col<uint32_t>{&S.vl[0][lane], kLanes}, o, n)
                                : decode_stream_slow(b, m, t, o, n));
