@@ -533,18 +533,23 @@ __device__ __forceinline__ int bare_block_len(const uint8_t *in, size_t in_len, 
 
 // the blocks of chunk c from x: count and exit (the first position at or
 // past the next chunk), or kBad; kWrite: their offsets to boff[base ...]
+// lst (walk only): the first kList block starts, relative to the chunk start
+constexpr int kList = 32;
 template <bool kExact, bool kWrite>
 __device__ __forceinline__ uint64_t bare_walk_chunk(const uint8_t *in, size_t in_len, size_t c,
                                                     uint64_t x, uint32_t &cnt,
                                                     uint64_t *boff, uint64_t base,
-                                                    uint64_t boff_cap = 0) {
+                                                    uint64_t boff_cap = 0,
+                                                    uint16_t *lst = nullptr) {
   cnt = 0;
   if (x == kNone || x == kBad) return kBad;
-  const uint64_t lim = 1 + (c + 1) * (uint64_t)kChunkB;
+  const uint64_t c0 = 1 + c * (uint64_t)kChunkB;
+  const uint64_t lim = c0 + kChunkB;
   while (x < lim && x < in_len) {
     const int L = bare_block_len<kExact>(in, in_len, x);
     if (L == 0) return kBad;
     if (kWrite && base + cnt < boff_cap) boff[base + cnt] = x - 1;
+    if (!kWrite && lst && cnt < (uint32_t)kList) lst[cnt] = (uint16_t)(x - c0);
     ++cnt;
     x += (uint64_t)L;
   }
@@ -559,12 +564,28 @@ __global__ __launch_bounds__(64) void lz4_bare_walk(const uint8_t *__restrict__ 
                                                     const uint64_t *__restrict__ cand,
                                                     uint32_t *__restrict__ cnt,
                                                     uint64_t *__restrict__ exitp,
-                                                    unsigned long long *__restrict__ gsum) {
+                                                    unsigned long long *__restrict__ gsum,
+                                                    uint16_t *__restrict__ lists,
+                                                    uint32_t *__restrict__ lok) {
+  // the lanes' lists are staged in LDS (a global store per block would make
+  // every next header load wait for it: in-order vmcnt) and leave as one
+  // coalesced 4 KB copy per wave
+  __shared__ alignas(16) uint16_t ls[64 * kList];
   const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
   uint32_t n = 0;
   if (c < nchunks) {
-    exitp[c] = bare_walk_chunk<kExact, false>(in, in_len, c, cand[c], n, nullptr, 0);
+    exitp[c] = bare_walk_chunk<kExact, false>(in, in_len, c, cand[c], n, nullptr, 0, 0,
+                                              ls + threadIdx.x * kList);
     cnt[c] = n;
+    lok[c] = n <= (uint32_t)kList ? 1u : 0u;   // the list holds every block start
+  }
+  __syncthreads();
+  {
+    const size_t c0 = (size_t)blockIdx.x * 64;
+    const int nl = (int)min((size_t)64, nchunks - c0);
+    uint4 *dst = reinterpret_cast<uint4 *>(lists + c0 * kList);
+    const uint4 *src = reinterpret_cast<const uint4 *>(ls);
+    for (int i = threadIdx.x; i < nl * kList / 8; i += 64) dst[i] = src[i];
   }
   unsigned long long t = n;
 #pragma unroll
@@ -605,7 +626,8 @@ __global__ __launch_bounds__(64) void lz4_bare_fix(const uint8_t *__restrict__ i
                                                    unsigned long long *__restrict__ gsum,
                                                    const unsigned int *__restrict__ nmis_p,
                                                    const unsigned int *__restrict__ mis,
-                                                   unsigned long long *__restrict__ status) {
+                                                   unsigned long long *__restrict__ status,
+                                                   uint32_t *__restrict__ lok) {
   __shared__ unsigned int list[kMisCap];
   const int lane = threadIdx.x;
   const unsigned int nmis = *nmis_p;
@@ -659,6 +681,7 @@ __global__ __launch_bounds__(64) void lz4_bare_fix(const uint8_t *__restrict__ i
       cand[f + 1] = e;
       cnt[f + 1] = n;
       exitp[f + 1] = ex;
+      lok[f + 1] = 0u;                               // its list is stale: re-walked for offsets
       atomicAdd(&gsum[(f + 1) / 64], (unsigned long long)n - (unsigned long long)old);
     }
     ov_c = f + 1;
@@ -708,7 +731,9 @@ __global__ __launch_bounds__(64) void lz4_bare_offsets(const uint8_t *__restrict
                                                        const uint32_t *__restrict__ cnt,
                                                        const unsigned long long *__restrict__ gbase,
                                                        uint64_t *__restrict__ boff,
-                                                       uint64_t boff_cap) {
+                                                       uint64_t boff_cap,
+                                                       const uint16_t *__restrict__ lists,
+                                                       const uint32_t *__restrict__ lok) {
   const size_t c = (size_t)blockIdx.x * 64 + threadIdx.x;
   const uint32_t v = c < nchunks ? cnt[c] : 0u;
   uint32_t x = v;
@@ -717,10 +742,38 @@ __global__ __launch_bounds__(64) void lz4_bare_offsets(const uint8_t *__restrict
     const uint32_t o = (uint32_t)__shfl_up((int)x, d, 64);
     if ((int)threadIdx.x >= d) x += o;
   }
-  if (c >= nchunks) return;
-  const uint64_t base = gbase[blockIdx.x] + x - v;
-  uint32_t n = 0;
-  bare_walk_chunk<kExact, true>(in, in_len, c, cand[c], n, boff, base, boff_cap);
+  // the wave's offsets are one contiguous range [wbase, wbase + total):
+  // staged in LDS and stored coalesced when they fit, else stored per lane
+  constexpr int kStageN = 1024;
+  __shared__ uint64_t st[kStageN];
+  const uint32_t total = (uint32_t)__shfl((int)x, 63, 64);
+  const uint64_t wbase = gbase[blockIdx.x];
+  const bool staged = total <= (uint32_t)kStageN;
+  if (c < nchunks) {
+    const uint32_t rel = x - v;
+    if (lok[c]) {
+      // the walk's list: no second walk of the chain (its loads wait on
+      // memory once per block)
+      const uint64_t c0 = 1 + c * (uint64_t)kChunkB;
+      const uint16_t *l = lists + c * kList;
+      for (uint32_t i = 0; i < v; ++i) {
+        const uint64_t o = c0 + l[i] - 1;
+        if (staged) st[rel + i] = o;
+        else if (wbase + rel + i < boff_cap) boff[wbase + rel + i] = o;
+      }
+    } else {
+      uint32_t n = 0;
+      if (staged)
+        bare_walk_chunk<kExact, true>(in, in_len, c, cand[c], n, st, rel, (uint64_t)kStageN);
+      else
+        bare_walk_chunk<kExact, true>(in, in_len, c, cand[c], n, boff, wbase + rel, boff_cap);
+    }
+  }
+  if (staged) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < total; i += 64)
+      if (wbase + i < boff_cap) boff[wbase + i] = st[i];
+  }
 }
 
 // One thread: the chain's verdict before any block is decoded -- 0 = go,
@@ -776,16 +829,17 @@ template <bool kExact>
 int bare_pass(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap, size_t nchunks,
               uint64_t *cand, uint32_t *cnt, uint64_t *exitp, unsigned long long *gsum,
               unsigned long long *gbase, unsigned long long *small, unsigned int *nmis,
-              unsigned int *mis, uint64_t *boff, size_t nb_cap, size_t *out_len, hipStream_t s) {
+              unsigned int *mis, uint16_t *lists, uint32_t *lok, uint64_t *boff, size_t nb_cap,
+              size_t *out_len, hipStream_t s) {
   const unsigned ng = (unsigned)((nchunks + 63) / 64);
   unsigned long long *d_nb = small, *d_status = small + 1, *d_res = small + 2, *d_gate = small + 4;
   hipLaunchKernelGGL(lz4_bare_walk<kExact>, dim3(ng), dim3(64), 0, s, in, in_len, nchunks, cand,
-                     cnt, exitp, gsum);
+                     cnt, exitp, gsum, lists, lok);
   if (hipMemsetAsync(nmis, 0, sizeof(unsigned int), s) != hipSuccess) return LZ4R_ERR_HIP;
   hipLaunchKernelGGL(lz4_bare_check, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s,
                      in_len, nchunks, cand, exitp, nmis, mis);
   hipLaunchKernelGGL(lz4_bare_fix<kExact>, dim3(1), dim3(64), 0, s, in, in_len, nchunks, cand, cnt,
-                     exitp, gsum, nmis, mis, d_status);
+                     exitp, gsum, nmis, mis, d_status, lok);
   hipLaunchKernelGGL(lz4_bare_scan, dim3(1), dim3(1024), 0, s, gsum, (size_t)ng, gbase, d_nb);
   uint64_t *own = nullptr;
   if (!boff) {
@@ -802,7 +856,7 @@ int bare_pass(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap, si
     boff = own;
   }
   hipLaunchKernelGGL(lz4_bare_offsets<kExact>, dim3(ng), dim3(64), 0, s, in, in_len, nchunks, cand,
-                     cnt, gbase, boff, (uint64_t)nb_cap);
+                     cnt, gbase, boff, (uint64_t)nb_cap, lists, lok);
   hipLaunchKernelGGL(lz4_bare_gate, dim3(1), dim3(1), 0, s, in, small, (uint64_t)nb_cap);
   hipLaunchKernelGGL(lz4_decode_blocks, dim3((unsigned)((nb_cap + kBPW - 1) / kBPW)),
                      dim3(kLanes), 0, s, in, in_len, static_cast<const uint64_t *>(boff), nb_cap,
@@ -842,10 +896,13 @@ extern "C" int lz4r_decompress_stream_device(const void *d_in, size_t in_len, vo
   const size_t nb_cap = nb_out <= nb_in ? nb_out : 0;
   // scratch: cand, exit (u64) per chunk; gsum, gbase per 64 chunks; 8 u64 of
   // nb, status, result[2], gate, the inconsistent-chunk count; the list
-  // (kMisCap u32); cnt (u32) per chunk; the block offsets (nb_cap u64)
+  // (kMisCap u32); cnt, list-valid (u32) and the first kList block starts
+  // (u16) per chunk; the block offsets (nb_cap u64)
   const size_t o_gsum = 16 * nchunks, o_small = o_gsum + 16 * ng, o_mis = o_small + 64;
   const size_t o_cnt = o_mis + 4 * (size_t)kMisCap;
-  const size_t o_boff = (o_cnt + 4 * nchunks + 7) & ~(size_t)7;
+  const size_t o_lok = o_cnt + 4 * nchunks;                  // u32 per chunk
+  const size_t o_lst = o_lok + 4 * nchunks;                  // kList u16 per chunk
+  const size_t o_boff = (o_lst + 2 * (size_t)kList * nchunks + 7) & ~(size_t)7;
   const size_t bytes = o_boff + 8 * nb_cap;
   uint8_t *scr = nullptr;
   if (hipMallocAsync(reinterpret_cast<void **>(&scr), bytes, s) != hipSuccess) return LZ4R_ERR_NOMEM;
@@ -857,18 +914,21 @@ extern "C" int lz4r_decompress_stream_device(const void *d_in, size_t in_len, vo
   unsigned int *nmis = reinterpret_cast<unsigned int *>(small + 5);
   unsigned int *mis = reinterpret_cast<unsigned int *>(scr + o_mis);
   uint32_t *cnt = reinterpret_cast<uint32_t *>(scr + o_cnt);
+  uint32_t *lok = reinterpret_cast<uint32_t *>(scr + o_lok);
+  uint16_t *lists = reinterpret_cast<uint16_t *>(scr + o_lst);
   uint64_t *boff = reinterpret_cast<uint64_t *>(scr + o_boff);
   hipLaunchKernelGGL(lz4_bare_cand, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, in,
                      in_len, nchunks, cand);
   // fast mode (block length = its size field); the exact mode parses every
   // block and is needed only for streams with truncated matches
   int rc = bare_pass<false>(in, in_len, out, out_cap, nchunks, cand, cnt, exitp, gsum, gbase,
-                            small, nmis, mis, nb_cap ? boff : nullptr, nb_cap, out_len, s);
+                            small, nmis, mis, lists, lok, nb_cap ? boff : nullptr, nb_cap,
+                            out_len, s);
   if (rc == LZ4R_ERR_CORRUPT) {
     hipLaunchKernelGGL(lz4_bare_cand, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, in,
                        in_len, nchunks, cand);
     rc = bare_pass<true>(in, in_len, out, out_cap, nchunks, cand, cnt, exitp, gsum, gbase, small,
-                         nmis, mis, nb_cap ? boff : nullptr, nb_cap, out_len, s);
+                         nmis, mis, lists, lok, nb_cap ? boff : nullptr, nb_cap, out_len, s);
   }
   (void)hipFreeAsync(scr, s);
   if (hipStreamSynchronize(s) != hipSuccess) return LZ4R_ERR_HIP;
