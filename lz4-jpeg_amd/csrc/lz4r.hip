@@ -174,6 +174,59 @@ __device__ __forceinline__ void xchg_rtn5(uint32_t (&old)[5], const uint32_t (&a
       : "memory");
 }
 
+// Empty the 1024 heads (4 KB at kHeadOff, LDS offset 368: TileLds is the
+// kernel's only LDS object) with ds_write_addtid_b32 (address = m0 + offset
+// + 4 lane, no address VGPR): 2 LDS cycles per 256 B against 13 per 1 KB for
+// ds_write_b128, whose cost is the transfer of its four data VGPRs.  m0 still
+// holds the previous block's sequence count (the walk's counter) until the
+// s_mov lands: without the wait state the first store went to m0_old + 368,
+// left stale heads whose chains could loop, and the kernel hung.
+__device__ __forceinline__ void head_reset_addtid() {
+  const uint32_t v = kNoLink;
+  asm volatile(
+      "s_mov_b32 m0, 0\n\t"
+      "s_nop 0\n\t"     // SALU write of m0 -> LDS add-TID read of m0: one wait state
+      "ds_write_addtid_b32 %0 offset:368\n\t"
+      "ds_write_addtid_b32 %0 offset:624\n\t"
+      "ds_write_addtid_b32 %0 offset:880\n\t"
+      "ds_write_addtid_b32 %0 offset:1136\n\t"
+      "ds_write_addtid_b32 %0 offset:1392\n\t"
+      "ds_write_addtid_b32 %0 offset:1648\n\t"
+      "ds_write_addtid_b32 %0 offset:1904\n\t"
+      "ds_write_addtid_b32 %0 offset:2160\n\t"
+      "ds_write_addtid_b32 %0 offset:2416\n\t"
+      "ds_write_addtid_b32 %0 offset:2672\n\t"
+      "ds_write_addtid_b32 %0 offset:2928\n\t"
+      "ds_write_addtid_b32 %0 offset:3184\n\t"
+      "ds_write_addtid_b32 %0 offset:3440\n\t"
+      "ds_write_addtid_b32 %0 offset:3696\n\t"
+      "ds_write_addtid_b32 %0 offset:3952\n\t"
+      "ds_write_addtid_b32 %0 offset:4208"
+      :
+      : "v"(v)
+      : "memory");
+}
+static_assert(kHeadOff == 368 && kH == 1024, "head_reset_addtid offsets");
+
+// Zero rec[0 .. 320) (1,280 B at kRecOff, the local(p) accumulators) the
+// same way: 5 add-TID stores instead of two ds_write2_b32 and a ds_write_b32
+// per lane.  Called after the heads' last exchange (rec[0 .. 192) lies under
+// the heads).
+__device__ __forceinline__ void rec_zero_addtid() {
+  asm volatile(
+      "s_mov_b32 m0, 0\n\t"
+      "s_nop 0\n\t"
+      "ds_write_addtid_b32 %0 offset:%c1\n\t"
+      "ds_write_addtid_b32 %0 offset:%c2\n\t"
+      "ds_write_addtid_b32 %0 offset:%c3\n\t"
+      "ds_write_addtid_b32 %0 offset:%c4\n\t"
+      "ds_write_addtid_b32 %0 offset:%c5"
+      :
+      : "v"(0u), "i"(kRecOff), "i"(kRecOff + 256), "i"(kRecOff + 512), "i"(kRecOff + 768),
+        "i"(kRecOff + 1024)
+      : "memory");
+}
+
 typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned LDS access (the LDS
                                                      // runs in unaligned mode; replayed)
 
@@ -296,12 +349,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   // 1024 u32 heads (4 KB) overlay the queue, the candidates and the front of
   // ent and rec -- all dead until the heads are (ent and rec are written
   // after the exchanges)
-  uint8_t *const sb = reinterpret_cast<uint8_t *>(&S);
-  static_assert(kH % 256 == 0 && kHeadOff == 368, "head reset: 16-B stores; asm offset");
-#pragma unroll
-  for (int i = 0; i < kH / 256; ++i)      // empty heads (the previous block's data)
-    reinterpret_cast<uint4 *>(sb + kHeadOff)[i * 64 + lane] =
-        make_uint4(kNoLink, kNoLink, kNoLink, kNoLink);
+  head_reset_addtid();                   // empty heads (the previous block's data)
   // Blocked layout: lane l owns the five positions p0 .. p0 + 4, p0 = 5 l
   // (lanes 60..63 own none of a 300-B block).  One 12-byte window per lane
   // gives all five 4-gram keys and preceding bytes; the five head swaps go
@@ -337,10 +385,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     }
     uint32_t old[5];
     xchg_rtn5(old, adr, set);
+    rec_zero_addtid();                   // local(p) accumulators (past n: unused)
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = p0 + r;
-      S.rec[p] = 0u;                    // local(p) accumulator (branch-free: past n unused)
       // the previous head: a byte link (kNoLink: none)
       const uint32_t link = old[r];
       // blk[p - 1]; 256 for p = 0, which so differs from every byte and makes
