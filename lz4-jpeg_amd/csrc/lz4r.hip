@@ -227,23 +227,32 @@ __device__ __forceinline__ void rec_zero_addtid() {
       : "memory");
 }
 
-typedef uint64_t u64u __attribute__((aligned(1)));   // unaligned LDS access (the LDS
-                                                     // runs in unaligned mode; replayed)
-
 // Longest common prefix of the byte runs at a and b (a < b), capped at
 // `limit` = n - b: the canonical clamp (a match never crosses the block end).
-// 8-byte words as unaligned ds_read_b64 (the LDS runs in unaligned mode;
-// an aligned-read + funnel-shift variant cut the LDS replays but cost more
-// VALU than it saved, and 8 bytes per step measured the same); reads past
-// the region land in its pad (>= 16 B past any block end).
+// Each operand's 16 bytes come from aligned dwords and v_alignbyte: a
+// misaligned ds_read_b128 is replayed at ~64 LDS cycles, and the kernel's
+// LDS array is ~80 % busy (SQ_LDS_IDX_ACTIVE), so the 4 extra VALU per
+// operand pay (-1 % lz4_tiles; an earlier 8-byte funnel-shift form cost ~30
+// VALU per block and lost).  Reads past the region land in its pad (>= 48 B
+// past any block end; the aligned form reads at most 19 past it).
 __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
   int l = 0;
   bool diff;
   do {                                    // 16 bytes per step, one exit condition
-    const uint64_t x0 = *reinterpret_cast<const u64u *>(d + a + l) ^
-                        *reinterpret_cast<const u64u *>(d + b + l);
-    const uint64_t x1 = *reinterpret_cast<const u64u *>(d + a + l + 8) ^
-                        *reinterpret_cast<const u64u *>(d + b + l + 8);
+    // 16 bytes at byte offset x from five aligned dwords (two ds_read2_b32 and
+    // a ds_read_b32: no misaligned replay), byte-aligned by v_alignbyte
+    auto at16 = [&](int x) {
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(d + (x & ~3));
+      const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+      const uint32_t sh = (uint32_t)(x & 3);
+      return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh),
+                        __builtin_amdgcn_alignbyte(w2, w1, sh),
+                        __builtin_amdgcn_alignbyte(w3, w2, sh),
+                        __builtin_amdgcn_alignbyte(w4, w3, sh));
+    };
+    const uint4 A = at16(a + l), B = at16(b + l);
+    const uint64_t x0 = ((uint64_t)(A.y ^ B.y) << 32) | (A.x ^ B.x);
+    const uint64_t x1 = ((uint64_t)(A.w ^ B.w) << 32) | (A.z ^ B.z);
     diff = (x0 | x1) != 0;
     // first differing byte, branch-free (a select, not an exec-masked if/else)
     const uint32_t a0 = (uint32_t)__builtin_ctzll(x0 | (1ull << 63)) >> 3;
@@ -463,6 +472,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     const uint8_t *const qb = reinterpret_cast<const uint8_t *>(S.q());
     uint8_t *const cb = reinterpret_cast<uint8_t *>(S.cand());
     int a = 0, b = 0;
+    uint32_t me = 0;                       // the walker's own entry (re-read only on a take)
     uint64_t vm = 0;                       // lanes holding a walker
     for (;;) {
       if (qrd4 < qwr4) {                   // (uniform) idle lanes take queued walkers
@@ -474,9 +484,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
         b = (int)sel_mask(nm_, it >> 16, (uint32_t)b);
         vm |= nm_;
         qrd4 += 4 * __popcll(em);
+        me = ent_at(a);                    // (lanes that kept their walker read the same word)
       }
       if (vm == 0) break;                  // no walker left and the queue is empty
-      const uint32_t me = ent_at(a), o = ent_at(b);
+      const uint32_t o = ent_at(b);
       const uint32_t x = me ^ o;
       // a ballot of each compare (a ballot of a combined bool costs two VALU)
       const uint64_t cm = vm & ballot((x & (31u << 17)) == 0) & ballot(x >= (1u << 22));
