@@ -227,6 +227,8 @@ def main(argv=None):
     ap.add_argument("--jpeg-steps", type=int, default=0, help="default: max(50, 10*steps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-jpeg", action="store_true")
+    ap.add_argument("--no-cfg4-share", action="store_true",
+                    help="skip the 8 GiB config-4 per-GPU share line at N = 1")
     ap.add_argument("--no-jpeg-batch", action="store_true",
                     help="skip the 128-image single-launch JPEG line at N = 1")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -448,6 +450,14 @@ def run_lz4(ctx, n_total, scaling):
             del full
         log(f"lz4 gather: {gather_ms:.2f} ms for {sum(lens) + 1} B")
 
+    # N = 1: one GPU's share of config 4 (the 8-GPU job's rank-0 shard: the
+    # first 8 GiB of the 64 GiB corpus) with the N > 1 step -- a segment
+    # compress and its length read back (the all_gather of one rank is that
+    # read) -- so the driver's 1 -> 8 curve has a same-work denominator
+    share = None
+    if world == 1 and not args.no_cfg4_share:
+        share = run_cfg4_share(ctx, comp)
+
     roof_lz4 = {
         "bound": "hbm", "kernel": "lz4_tiles",
         "achieved": round(n / (avg_match_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
@@ -493,8 +503,57 @@ def run_lz4(ctx, n_total, scaling):
         "lz4_gather_ok": gather_ok,
         "value_incl_gather": (None if gather_ms is None else
                               round(n_total / ((lz4_ms + gather_ms) / 1e3) / 1e9, 3)),
+        "value_per_gpu": round(lz4_gbs / world, 3),
+        "cfg4_share": share,
         "lz4_decode": lz4_dec,
     }
+
+
+def run_cfg4_share(ctx, comp):
+    """configs[3]'s per-GPU work at 8 GPUs on this one GPU: the 8 GiB shard
+    [0, 8 GiB) of the 64 GiB corpus, compressed as a segment per step."""
+    torch = ctx.torch
+    from lz4jpeg import dist as ldist
+    from lz4jpeg import lz4, synth
+    args, dev = ctx.args, ctx.dev
+    world8 = 8
+    lo, hi = ldist.shard_bytes(CFG4_BYTES, world8, 0)
+    n = hi - lo
+    d_in = torch.empty(n + 16, dtype=torch.uint8, device=dev)
+    synth.random_passages_device(d_in, n, length=30000, seed=1, first=lo)
+    cap = n + n // 8 + (1 << 20)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    d_len = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step():
+        comp.compress_async(d_in, n, d_out, d_len, segment=True, final_shard=False)
+        return int(d_len.item())
+
+    for _ in range(max(1, args.warmup)):
+        seg = step()
+    if seg > cap:
+        raise RuntimeError(f"lz4 cfg4 share: segment {seg} B exceeds {cap} B")
+    torch.cuda.synchronize()
+    comp.set_timing(True)
+    tiles = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        seg = step()
+        tiles.append(comp.last_timing()[1])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    comp.set_timing(False)
+    del d_in, d_out
+    res = {
+        "metric": "LZ4 compress GB/s of one GPU's share of configs[3] (8 GPUs)",
+        "value": round(n / (dt / args.steps) / 1e9, 3), "unit": "GB/s",
+        "ms_per_step": round(dt / args.steps * 1e3, 4), "steps": args.steps,
+        "bytes": n, "segment_bytes": seg, "lz4_tiles_ms": round(sum(tiles) / len(tiles), 4),
+        "step": "segment compress (lz4r_compress_segment_async) + length read-back",
+        "note": "the 8-GPU job's rank-0 shard [0, 8 GiB) of the 64 GiB corpus; x8 is the "
+                "ideal 8-GPU configs[3] value (no scaling loss)"}
+    log(f"lz4 cfg4 share: {res['ms_per_step']} ms/step, {res['value']} GB/s")
+    return res
 
 
 def run_jpeg(ctx, total_images, scaling):
@@ -541,6 +600,7 @@ def run_jpeg(ctx, total_images, scaling):
     jres = {
         "metric": "JPEG DCT+quant+zigzag Gpixel/s (bit-exact int16 coefficients)",
         "value": round(gpix, 3), "unit": "Gpixel/s", "n_gpus": world, "steps": jsteps,
+        "value_per_gpu": round(gpix / world, 3),
         "ms_per_step": round(jdt / jsteps * 1e3, 4), "higher_is_better": True,
         "scaling": scaling, "dtype": "f64",
         "data": "synthetic: glibc rand() RGBA noise (random_image.c) from srand(1), images "

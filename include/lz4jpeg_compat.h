@@ -77,11 +77,15 @@ void LZ4_decode(char *input_bin_file, char *log);
 /* find_longest_match <- LZ4.c:290-323.  The longest match at current_index
  * of the block starting at `input` (earliest source among equals), as
  * (uint8_t)len with *match_distance set, or 0 when len < 4.  The block is
- * the one block_encode is encoding (its block_length), otherwise the 300
- * bytes at input (DEFAULT_BLOCK_LENGTH, LZ4.c:22); matches are clamped at
- * the block end (the reference reads past it).  GPU: the
- * first call for a block computes every position of it in one launch
- * (lz4r_block_matches_device); later calls on the same bytes are lookups. */
+ * the one block_encode is encoding (its block_length, any length), otherwise
+ * the 300 bytes at input (DEFAULT_BLOCK_LENGTH, LZ4.c:23: a standalone call
+ * needs 300 readable bytes there, as the reference reads up to
+ * MAX_MATCH_LENGTH past current_index); matches are clamped at the block end
+ * (the reference reads past it).  GPU: the first call for a
+ * block computes every position of it in one launch
+ * (lz4r_block_matches_device; lz4r_window_matches_device with the 65535-byte
+ * window for a block longer than 300); later calls on the same bytes are
+ * lookups. */
 uint8_t find_longest_match(uint8_t *input, size_t current_index, uint16_t *match_distance);
 
 /* block_encode <- LZ4.c:506-620: the greedy parse of one block into `block`

@@ -99,6 +99,14 @@ int lz4r_compress_segment_async(lz4r_ctx *ctx, const void *d_in, size_t n,
  * value is len & 0xFF. */
 int lz4r_block_matches_device(const void *d_in, size_t n, void *d_matches, void *stream);
 
+/* find_longest_match (LZ4.c:290-323) at every position of ONE block of any
+ * length n (what block_encode does for a block_length other than 300): the
+ * reference's whole window (sources i >= p - WINDOW_SIZE, LZ4.c:295), match
+ * length capped at MAX_MATCH_LENGTH (1024, LZ4.c:20) and at the block end.
+ * d_matches[p] = len | dist << 16, or 0 when len < 4.  O(n * min(n, 65535))
+ * work: a compatibility path.  Asynchronous on `stream`; n < 2^32. */
+int lz4r_window_matches_device(const void *d_in, size_t n, void *d_matches, void *stream);
+
 /* After a compress call: copy the encoded byte count (uint16) of each of the
  * first `count` blocks of the last call to `dst` (host or device memory),
  * then synchronise `stream`.  Block b's bytes start at sum(sizes[0..b)) after

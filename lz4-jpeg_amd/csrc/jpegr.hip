@@ -110,7 +110,8 @@ template <bool RAW>
 __global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
     const uint8_t *__restrict__ rgba, int w, int h, int tiles_x, int tiles_y,
     int strips, void *__restrict__ out) {
-  __shared__ double ylds[kTiles * kYStride];
+  // 16-B aligned: phase 4 reads the int16 output staged over it as uint4
+  __shared__ alignas(16) double ylds[kTiles * kYStride];
   __shared__ double crl[kTiles * kCStride];
   __shared__ double cbl[kTiles * kCStride];
   // the strip's int16 output is staged over the luma samples once every

@@ -621,7 +621,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
         "s_mov_b32 %4, m0"
         : "+v"(seqv), "+s"(w), "+v"(va), "=&v"(vt), "=s"(it)
         : "s"((uint32_t)n4 << 17), "i"(kRecOff)
-        : "scc", "memory");   // (m0 is reserved: no other use in this kernel)
+        : "scc", "memory");
   }
   // Past 64 sequences (only with truncated matches) the walk is redone into S.seq.
   const bool slow = it > 64;
@@ -742,6 +742,41 @@ __global__ __launch_bounds__(64) void lz4_matches(const uint8_t *__restrict__ in
   if (lane < 16) S.buf[kInOff + n + lane] = 0;
   wave_sync();
   encode_block<true>(S, n, mout + (size_t)t * kBlk, nullptr);
+}
+
+// find_longest_match over a block of any length n (block_encode with a
+// block_length other than 300): the reference's whole window, LZ4.c:295-312
+// -- sources i in [max(0, p - WINDOW_SIZE), p), match length capped at
+// MAX_MATCH_LENGTH (1024) and, canonically, at the block end n - p; the
+// longest wins, ties to the smallest i (strict '>', LZ4.c:307).  One wave
+// per position, its lanes striding over the window, a max-reduction of
+// len << 17 | dist (the larger dist is the smaller source).  A compatibility
+// path, O(n * window): the 300-byte blocks of the compressor use lz4_tiles.
+constexpr int kWindow = 65535;          // WINDOW_SIZE, LZ4.c:22
+constexpr int kMaxMatch = 1024;         // MAX_MATCH_LENGTH, LZ4.c:20
+
+__global__ __launch_bounds__(256) void lz4_window_matches(const uint8_t *__restrict__ in,
+                                                          uint32_t n, uint32_t p_first,
+                                                          uint32_t *__restrict__ mout) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t p = p_first + blockIdx.x * 4u + (threadIdx.x >> 6);
+  if (p >= n) return;
+  const uint32_t cap = min((uint32_t)kMaxMatch, n - p);
+  const uint32_t i0 = p >= (uint32_t)kWindow ? p - (uint32_t)kWindow : 0u;
+  const uint8_t c0 = in[p];
+  uint32_t best = 0;
+  for (uint32_t i = i0 + (uint32_t)lane; i < p; i += 64) {
+    if (in[i] != c0) continue;
+    uint32_t l = 1;
+    while (l < cap && in[i + l] == in[p + l]) ++l;
+    best = max(best, (l << 17) | (p - i));
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, d, 64));
+  if (lane == 0) {
+    const uint32_t len = best >> 17;
+    mout[p] = len >= 4 ? len | ((best & 0x1FFFFu) << 16) : 0u;   // MIN_MATCH_LENGTH, LZ4.c:314
+  }
 }
 
 // ---- placement: exclusive scan of tile sizes, then gather -----------------
@@ -1279,13 +1314,31 @@ int lz4r_compress_device(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, s
 }
 
 int lz4r_block_matches_device(const void *d_in, size_t n, void *d_matches, void *stream) {
-  if (!d_in || !d_matches || n == 0) return LZ4R_ERR_ARG;
+  if (!d_in || !d_matches || n == 0 || n > kMaxInput) return LZ4R_ERR_ARG;
   const size_t nb = (n + kBlk - 1) / kBlk;
-  if (nb > 0x7fffffffULL) return LZ4R_ERR_ARG;
-  hipLaunchKernelGGL(lz4_matches, dim3((unsigned)nb), dim3(64), 0,
-                     static_cast<hipStream_t>(stream), static_cast<const uint8_t *>(d_in),
-                     (uint32_t)nb, (uint32_t)(n - (nb - 1) * kBlk),
-                     static_cast<uint32_t *>(d_matches));
+  const uint8_t *in = static_cast<const uint8_t *>(d_in);
+  uint32_t *mo = static_cast<uint32_t *>(d_matches);
+  // a grid of 64-lane workgroups stays under HIP's 2^32 work-items: launch
+  // chunks of kChunk blocks, as run() does
+  for (size_t b0 = 0; b0 < nb; b0 += kChunk) {
+    const size_t nbc = std::min(kChunk, nb - b0);
+    const uint32_t last_n = (uint32_t)(b0 + nbc == nb ? n - (nb - 1) * kBlk : kBlk);
+    hipLaunchKernelGGL(lz4_matches, dim3((unsigned)nbc), dim3(64), 0,
+                       static_cast<hipStream_t>(stream), in + b0 * kBlk, (uint32_t)nbc, last_n,
+                       mo + b0 * kBlk);
+  }
+  return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
+}
+
+int lz4r_window_matches_device(const void *d_in, size_t n, void *d_matches, void *stream) {
+  if (!d_in || !d_matches || n == 0 || n > 0xFFFFFFFFull) return LZ4R_ERR_ARG;
+  constexpr size_t kPosChunk = size_t(1) << 26;       // 2^24 workgroups of 256 per launch
+  for (size_t p0 = 0; p0 < n; p0 += kPosChunk) {
+    const size_t np = std::min(kPosChunk, n - p0);
+    hipLaunchKernelGGL(lz4_window_matches, dim3((unsigned)((np + 3) / 4)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), static_cast<const uint8_t *>(d_in),
+                       (uint32_t)n, (uint32_t)p0, static_cast<uint32_t *>(d_matches));
+  }
   return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
 }
 

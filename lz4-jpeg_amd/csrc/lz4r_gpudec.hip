@@ -900,9 +900,11 @@ extern "C" int lz4r_decompress_stream_device(const void *d_in, size_t in_len, vo
   // (u16) per chunk; the block offsets (nb_cap u64)
   const size_t o_gsum = 16 * nchunks, o_small = o_gsum + 16 * ng, o_mis = o_small + 64;
   const size_t o_cnt = o_mis + 4 * (size_t)kMisCap;
-  const size_t o_lok = o_cnt + 4 * nchunks;                  // u32 per chunk
-  const size_t o_lst = o_lok + 4 * nchunks;                  // kList u16 per chunk
-  const size_t o_boff = (o_lst + 2 * (size_t)kList * nchunks + 7) & ~(size_t)7;
+  // every region 16-B aligned: lz4_bare_walk stores the lists as uint4
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t o_lok = al16(o_cnt + 4 * nchunks);            // u32 per chunk
+  const size_t o_lst = al16(o_lok + 4 * nchunks);            // kList u16 per chunk
+  const size_t o_boff = al16(o_lst + 2 * (size_t)kList * nchunks);
   const size_t bytes = o_boff + 8 * nb_cap;
   uint8_t *scr = nullptr;
   if (hipMallocAsync(reinterpret_cast<void **>(&scr), bytes, s) != hipSuccess) return LZ4R_ERR_NOMEM;

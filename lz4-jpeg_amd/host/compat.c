@@ -97,33 +97,57 @@ void lz4_encode(void) {
 /* ---- per-block API: find_longest_match / block_encode / write_output ---- */
 
 /* The block find_longest_match answers for: its bytes, and every position's
- * len | dist << 16 from one lz4r_block_matches_device launch.  Per thread. */
+ * len | dist << 16 from one launch -- lz4r_block_matches_device for a
+ * 300-byte (or shorter) block, lz4r_window_matches_device (the reference's
+ * whole 65535-byte window, MAX_MATCH_LENGTH 1024) for a longer block_length.
+ * Host and device buffers grow to the block; per thread. */
 static __thread struct {
   const uint8_t *ptr;
-  size_t n;
-  uint8_t bytes[LZ4R_BLOCK];
-  uint32_t match[LZ4R_BLOCK];
+  size_t n, cap;
+  uint8_t *bytes;
+  uint32_t *match;
   int valid;
   void *d_in, *d_match;
 } fm_cache;
 static __thread size_t fm_block_length;   /* set while block_encode runs */
 
+static void fm_reserve(size_t n) {
+  if (n <= fm_cache.cap) return;
+  free(fm_cache.bytes);
+  free(fm_cache.match);
+  (void)hipFree(fm_cache.d_in);
+  (void)hipFree(fm_cache.d_match);
+  fm_cache.bytes = (uint8_t *)malloc(n);
+  fm_cache.match = (uint32_t *)malloc(n * sizeof(uint32_t));
+  fm_cache.d_in = fm_cache.d_match = NULL;
+  fm_cache.valid = 0;
+  fm_cache.cap = 0;
+  if (!fm_cache.bytes || !fm_cache.match) {
+    perror("Error: Unable to allocate memory");
+    exit(1);
+  }
+  /* +16: the block kernel's staging may read a few bytes past a short block */
+  if (hipMalloc(&fm_cache.d_in, n + 16) != hipSuccess ||
+      hipMalloc(&fm_cache.d_match, n * sizeof(uint32_t)) != hipSuccess)
+    die_hip("hipMalloc", LZ4R_ERR_NOMEM);
+  fm_cache.cap = n;
+}
+
 static void fm_load(const uint8_t *input, size_t n) {
   if (fm_cache.valid && fm_cache.ptr == input && fm_cache.n == n &&
       memcmp(fm_cache.bytes, input, n) == 0)
     return;
-  if (!fm_cache.d_in &&
-      (hipMalloc(&fm_cache.d_in, LZ4R_BLOCK + 16) != hipSuccess ||
-       hipMalloc(&fm_cache.d_match, LZ4R_BLOCK * sizeof(uint32_t)) != hipSuccess))
-    die_hip("hipMalloc", LZ4R_ERR_NOMEM);
+  fm_reserve(n < LZ4R_BLOCK ? LZ4R_BLOCK : n);
   int rc = LZ4R_OK;
   if (hipMemcpy(fm_cache.d_in, input, n, hipMemcpyHostToDevice) != hipSuccess) rc = LZ4R_ERR_HIP;
-  if (rc == LZ4R_OK) rc = lz4r_block_matches_device(fm_cache.d_in, n, fm_cache.d_match, NULL);
+  if (rc == LZ4R_OK)
+    rc = n <= LZ4R_BLOCK ? lz4r_block_matches_device(fm_cache.d_in, n, fm_cache.d_match, NULL)
+                         : lz4r_window_matches_device(fm_cache.d_in, n, fm_cache.d_match, NULL);
   if (rc == LZ4R_OK &&
       hipMemcpy(fm_cache.match, fm_cache.d_match, n * sizeof(uint32_t), hipMemcpyDeviceToHost) !=
           hipSuccess)
     rc = LZ4R_ERR_HIP;
-  if (rc != LZ4R_OK) die_hip("lz4r_block_matches_device", rc);
+  if (rc != LZ4R_OK) die_hip("find_longest_match", rc);
   fm_cache.ptr = input;
   fm_cache.n = n;
   memcpy(fm_cache.bytes, input, n);
@@ -131,6 +155,7 @@ static void fm_load(const uint8_t *input, size_t n) {
 }
 
 uint8_t find_longest_match(uint8_t *input, size_t current_index, uint16_t *match_distance) {
+  /* inside block_encode: its block; standalone: the 300 bytes at input */
   const size_t n = fm_block_length ? fm_block_length : LZ4R_BLOCK;
   if (current_index >= n) return 0;
   fm_load(input, n);

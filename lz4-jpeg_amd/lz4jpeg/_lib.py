@@ -28,6 +28,7 @@ SIGNATURES = [
     ("lz4r_copy_block_offsets", _i, [_vp, _vp, _c_size, _vp]),
     ("lz4r_block_offsets_device", _i, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_c_size)]),
     ("lz4r_block_matches_device", _i, [_vp, _c_size, _vp, _vp]),
+    ("lz4r_window_matches_device", _i, [_vp, _c_size, _vp, _vp]),
     ("lz4r_compress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
     ("lz4r_decompress", _i, [_vp, _c_size, _vp, _c_size, ctypes.POINTER(_c_size)]),
     ("lz4r_decompress_device", _i, [_vp, _c_size, _vp, _c_size, _vp, _c_size, _vp, _vp]),

@@ -83,10 +83,15 @@ class Compressor:
         return d_out, got.value
 
     def compress_async(self, d_in, n, d_out, d_len, stream=None, segment=False,
-                       final_shard=True):
+                       final_shard=None):
         """Enqueue only; the uint64 length lands in d_len (1-element int64 tensor).
-        segment=True: whole blocks without the frame header (one shard); a
-        non-final shard (final_shard=False) must be a multiple of 300 bytes."""
+        segment=True: whole blocks without the frame header (one shard);
+        final_shard must then be given: only the globally last shard may end
+        in a short block, a non-final shard (final_shard=False) must be a
+        multiple of 300 bytes (else the concatenated stream would differ from
+        the single-GPU one)."""
+        if segment and final_shard is None:
+            raise ValueError("compress_async(segment=True) needs final_shard=True/False")
         L = _lib.lib()
         args = (self._h, ctypes.c_void_p(d_in.data_ptr()), n, ctypes.c_void_p(d_out.data_ptr()),
                 d_out.numel(), ctypes.c_void_p(d_len.data_ptr()))

@@ -77,3 +77,16 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.LibraryMissing):
         _lib.lib()
+
+
+def test_match_finders_reject_bad_arguments_before_device():
+    """lz4r_block_matches_device launches in chunks of 2^24 blocks (HIP's
+    2^32 work-item grid limit); what it cannot take -- NULL, empty, above the
+    2^40-byte call limit -- is an argument error, found before any HIP call."""
+    L = _lib.lib()
+    p = ctypes.c_void_p(16)          # never dereferenced: every case fails first
+    assert L.lz4r_block_matches_device(None, 300, p, None) == _lib.LZ4R_ERR_ARG
+    assert L.lz4r_block_matches_device(p, 0, p, None) == _lib.LZ4R_ERR_ARG
+    assert L.lz4r_block_matches_device(p, (1 << 40) + 1, p, None) == _lib.LZ4R_ERR_ARG
+    assert L.lz4r_window_matches_device(p, 0, p, None) == _lib.LZ4R_ERR_ARG
+    assert L.lz4r_window_matches_device(p, 1 << 32, p, None) == _lib.LZ4R_ERR_ARG

@@ -169,3 +169,53 @@ def test_find_longest_match_every_position(gpu, oracle):
                 assert (m, d.value) == (best & 0xFF, bd), (trial, p)
             else:
                 assert m == 0, (trial, p)
+
+
+def _oracle_block(oracle, data):
+    """[u8 1] + the oracle's block_encode/write_block bytes of one block of
+    any length (lz4o_encode_block: the 65535-byte window, MAX_MATCH 1024)."""
+    out = ctypes.create_string_buffer(3 * len(data) + 64)
+    n = oracle.L.lz4o_encode_block(bytes(data), len(data), out)
+    return b"\x01" + out.raw[:n]
+
+
+@pytest.mark.parametrize("n", [301, 1000, 5000, 70000])
+def test_block_encode_longer_than_300(gpu, oracle, tmp_path, n):
+    """block_encode accepts any block_length (LZ4.c:506; the reference's
+    window is 65535 bytes, LZ4.c:22/295): blocks past 300 B take the
+    whole-window GPU match finder; 70,000 B crosses the window."""
+    text = golden_inputs.lz4_input("metamorphosis_spaces")
+    data = (text * (n // len(text) + 1))[:n]      # repeats the book: long matches
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(bytes(data), n)
+    frame = LZ4Frame(0, None)
+    blk = LZ4Block()
+    L.block_encode(ctypes.addressof(buf), n, ctypes.byref(blk), None, None, ctypes.byref(frame))
+    c = _libc()
+    path = tmp_path / "long.bin"
+    f = c.fopen(str(path).encode(), b"wb")
+    L.write_output(ctypes.byref(frame), f)
+    c.fclose(f)
+    assert path.read_bytes() == _oracle_block(oracle, data)
+
+
+def test_find_longest_match_standalone_short_block_then_long(gpu, oracle):
+    """The per-thread cache grows: a 300-B standalone call, then a 2,000-B
+    block_encode, then a 300-B block again (each answered for its own
+    bytes)."""
+    L = _lib.lib()
+    text = golden_inputs.lz4_input("metamorphosis_spaces")
+    a = ctypes.create_string_buffer(text[:300], 300)
+    d = ctypes.c_uint16(0)
+    first = [(L.find_longest_match(ctypes.addressof(a), p, ctypes.byref(d)), d.value)
+             for p in range(300)]
+    long_ = (text * 2)[:2000]
+    b = ctypes.create_string_buffer(long_, 2000)
+    frame = LZ4Frame(0, None)
+    blk = LZ4Block()
+    L.block_encode(ctypes.addressof(b), 2000, ctypes.byref(blk), None, None, ctypes.byref(frame))
+    assert frame.blocks == 1
+    again = [(L.find_longest_match(ctypes.addressof(a), p, ctypes.byref(d)), d.value)
+             for p in range(300)]
+    assert [m for m, _ in again] == [m for m, _ in first]
+    assert [dd for m, dd in again if m] == [dd for m, dd in first if m]
