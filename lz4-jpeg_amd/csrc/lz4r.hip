@@ -8,29 +8,34 @@
 // Blocks are independent; the compressor is one compute kernel, a scan and
 // an emission pass:
 //
-// lz4_tiles: workgroup = one wave = one 300-B block (5.1 KB of LDS, <= 64
+// lz4_tiles: workgroup = one wave = one 300-B block (4,976 B of LDS, <= 64
 // VGPRs -> 8 waves per SIMD; occupancy is what this LDS- and issue-bound
 // kernel lives on).  Per block:
 //   stage    the block's 75 dwords -> LDS (the only read of the input).
-//   position-parallel, blocked (lane l owns p = 5 l .. 5 l + 4):
-//     index  per-bucket chains of the 4-gram starts by a 10-bit hash: p
-//            exchanges itself into its bucket's u32 head (ds_wrxchg_rtn_b32)
-//            and keeps the old head as its link (byte offsets 4 p);
-//            entry = link | tag << 17 | preceding byte << 22.
-//     local  every unordered pair of a bucket is met once, by the later-
-//            inserted entry walking its chain; a lane keeps its walker until
-//            the chain ends and then takes the next queued one.  A pair
-//            (j < p) is a candidate when the tags agree and it is
-//            LEFT-MAXIMAL (j == 0 or blk[j-1] != blk[p-1]); a balanced lcp
-//            pass takes the longest candidate per p, ties to the smallest j
-//            (LDS atomicMax).
+//   position-major (lane l owns p = 64 r + l, r = 0..4):
+//     index  per-bucket chains of the 4-gram starts by a 10-bit hash: each
+//            position empties its bucket's u32 head, then exchanges itself
+//            into it (ds_wrxchg_rtn_b32) in ascending position order and keeps
+//            the old head as its link (byte offsets 4 p), so every chain
+//            strictly decreases; entry = link | (p == 0) << 15 | preceding
+//            byte << 16 | tag << 24, stored by add-TID (address = lane).
+//     local  every unordered pair of a bucket is met once, by the later
+//            position walking its chain (deepest walkers first); a lane
+//            keeps its walker until the chain ends -- or a link fails to
+//            decrease: the walk ends on any input -- and then takes the next
+//            queued one.  A pair (j < p) is a candidate when the tags agree
+//            and it is LEFT-MAXIMAL (j == 0 or blk[j-1] != blk[p-1]): one
+//            v_xad + one compare of the two entries; a balanced lcp pass over
+//            the 4-gram keys takes the longest candidate per p, ties to the
+//            smallest j (LDS atomicMax).
+//   blocked (lane l owns p = 5 l .. 5 l + 4):
 //     best   a candidate that is not left-maximal is the pair (j-1, p-1)
 //            shifted by one, whose match is one byte longer.  Hence
 //              best(p) = lexmax over q <= p of (q + local_len(q), q - local_j(q))
 //            i.e. the longest match ends furthest right and, among equals,
-//            has the largest distance (= smallest source, LZ4.c:307).  One
-//            wave max-scan gives best() for all p.  M = len & 0xFF (the
-//            uint8_t return, LZ4.c:317).
+//            has the largest distance (= smallest source, LZ4.c:307).  A
+//            running max over the lane's five and one wave max-scan give
+//            best() for all p.  M = len & 0xFF (the uint8_t return, LZ4.c:317).
 //     parse  nm(x) = first matchable position >= x; succ(c) = nm(c + M(c));
 //            the greedy parse (LZ4.c:516-583) is the walk c0 = nm(0),
 //            c_{k+1} = succ(c_k), one LDS read per sequence.
@@ -64,6 +69,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <type_traits>
 #include <new>
 #include <vector>
 
@@ -73,7 +79,8 @@
 // DESIGN.md, compiled only by tools/build_variants.sh into tools/variants/
 // (the Makefile's product build never defines it): 1 = no match search,
 // 2 = no index/match phase, 3 = index only (no candidates), 4 = candidates
-// without the lcp verification, 11 = no sequence emission.
+// without the lcp verification, 5 = the lcp without its result (no
+// matches downstream), 11 = no sequence emission.
 #ifndef LZ4R_VARIANT
 #define LZ4R_VARIANT 0
 #endif
@@ -88,6 +95,10 @@ __device__ unsigned long long lz4r_prof_acc[16];
     if (threadIdx.x == 0) atomicAdd(&lz4r_prof_acc[k], prof_n - prof_t); \
     prof_t = prof_n;                                                     \
   } while (0)
+#elif defined(LZ4R_MARK)
+// static phase markers in the assembly (tools: per-phase instruction counts)
+#define PROF_DECL
+#define PROF_MARK(k) asm volatile(";PHASE_END " #k ::: "memory")
 #else
 #define PROF_DECL
 #define PROF_MARK(k) \
@@ -143,7 +154,7 @@ struct TileLds {
     uint32_t nm[kArr];    // then: first matchable position >= x (dwords: no sub-dword LDS access)
   };
   uint32_t rec[kArr];     // local(p) accumulator; then dist | M<<9 | succ<<17
-  // chain walkers, walker | next chain entry << 16 (candidate phase)
+  // chain walkers: the walker's byte offset 4 p (candidate phase)
   __device__ __forceinline__ uint32_t *q() { return reinterpret_cast<uint32_t *>(buf + kQOff); }
   // per sequence, its match start (slow walk only)
   __device__ __forceinline__ uint32_t *seq() { return reinterpret_cast<uint32_t *>(buf + kQOff); }
@@ -159,9 +170,19 @@ static_assert(kRecOff + 4 * kArr <= 4976, "LDS of one wave");
 // The addresses are relative to the head array (kHeadOff, the instruction's
 // offset field); the LDS serves one wave's operations in order, so a later
 // exchange of the same head sees the earlier.
+// Each head this block uses is first emptied by the positions that hash to
+// it (five ds_write_b32 of kNoLink, before any exchange; the LDS serves one
+// wave's operations in order): a head no position of the block maps to is
+// never read, so the other ~800 of the 1024 need no reset (5 scattered
+// stores instead of 16 ds_write_addtid_b32 over the whole 4 KB).
 __device__ __forceinline__ void xchg_rtn5(uint32_t (&old)[5], const uint32_t (&a)[5],
                                           const uint32_t (&v)[5]) {
   asm volatile(
+      "ds_write_b32 %5, %15 offset:368\n\t"
+      "ds_write_b32 %6, %15 offset:368\n\t"
+      "ds_write_b32 %7, %15 offset:368\n\t"
+      "ds_write_b32 %8, %15 offset:368\n\t"
+      "ds_write_b32 %9, %15 offset:368\n\t"
       "ds_wrxchg_rtn_b32 %0, %5, %10 offset:368\n\t"
       "ds_wrxchg_rtn_b32 %1, %6, %11 offset:368\n\t"
       "ds_wrxchg_rtn_b32 %2, %7, %12 offset:368\n\t"
@@ -170,61 +191,58 @@ __device__ __forceinline__ void xchg_rtn5(uint32_t (&old)[5], const uint32_t (&a
       "s_waitcnt lgkmcnt(0)"
       : "=&v"(old[0]), "=&v"(old[1]), "=&v"(old[2]), "=&v"(old[3]), "=&v"(old[4])
       : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]),
-        "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4])
+        "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(kNoLink)
       : "memory");
 }
 
-// Empty the 1024 heads (4 KB at kHeadOff, LDS offset 368: TileLds is the
-// kernel's only LDS object) with ds_write_addtid_b32 (address = m0 + offset
-// + 4 lane, no address VGPR): 2 LDS cycles per 256 B against 13 per 1 KB for
-// ds_write_b128, whose cost is the transfer of its four data VGPRs.  m0 still
-// holds the previous block's sequence count (the walk's counter) until the
-// s_mov lands: without the wait state the first store went to m0_old + 368,
-// left stale heads whose chains could loop, and the kernel hung.
-__device__ __forceinline__ void head_reset_addtid() {
-  const uint32_t v = kNoLink;
-  asm volatile(
-      "s_mov_b32 m0, 0\n\t"
-      "s_nop 0\n\t"     // SALU write of m0 -> LDS add-TID read of m0: one wait state
-      "ds_write_addtid_b32 %0 offset:368\n\t"
-      "ds_write_addtid_b32 %0 offset:624\n\t"
-      "ds_write_addtid_b32 %0 offset:880\n\t"
-      "ds_write_addtid_b32 %0 offset:1136\n\t"
-      "ds_write_addtid_b32 %0 offset:1392\n\t"
-      "ds_write_addtid_b32 %0 offset:1648\n\t"
-      "ds_write_addtid_b32 %0 offset:1904\n\t"
-      "ds_write_addtid_b32 %0 offset:2160\n\t"
-      "ds_write_addtid_b32 %0 offset:2416\n\t"
-      "ds_write_addtid_b32 %0 offset:2672\n\t"
-      "ds_write_addtid_b32 %0 offset:2928\n\t"
-      "ds_write_addtid_b32 %0 offset:3184\n\t"
-      "ds_write_addtid_b32 %0 offset:3440\n\t"
-      "ds_write_addtid_b32 %0 offset:3696\n\t"
-      "ds_write_addtid_b32 %0 offset:3952\n\t"
-      "ds_write_addtid_b32 %0 offset:4208"
-      :
-      : "v"(v)
-      : "memory");
-}
-static_assert(kHeadOff == 368 && kH == 1024, "head_reset_addtid offsets");
+static_assert(kHeadOff == 368 && kH == 1024, "xchg_rtn5 offsets");
 
-// Zero rec[0 .. 320) (1,280 B at kRecOff, the local(p) accumulators) the
-// same way: 5 add-TID stores instead of two ds_write2_b32 and a ds_write_b32
-// per lane.  Called after the heads' last exchange (rec[0 .. 192) lies under
-// the heads).
-__device__ __forceinline__ void rec_zero_addtid() {
+// ent[64 r + lane] = e[r] (the position-major entries, r = 0..4) and zero
+// rec[0 .. 320) (1,280 B at kRecOff, the local(p) accumulators) with
+// ds_write_addtid_b32: 10 stores of 2 LDS cycles each, one m0 set.  Called
+// after the heads' last exchange (ent and rec[0 .. 192) lie under the heads).
+__device__ __forceinline__ void ent_store_rec_zero_addtid(const uint32_t (&e)[5]) {
   asm volatile(
       "s_mov_b32 m0, 0\n\t"
       "s_nop 0\n\t"
-      "ds_write_addtid_b32 %0 offset:%c1\n\t"
-      "ds_write_addtid_b32 %0 offset:%c2\n\t"
-      "ds_write_addtid_b32 %0 offset:%c3\n\t"
-      "ds_write_addtid_b32 %0 offset:%c4\n\t"
-      "ds_write_addtid_b32 %0 offset:%c5"
+      "ds_write_addtid_b32 %0 offset:%c6\n\t"
+      "ds_write_addtid_b32 %1 offset:%c7\n\t"
+      "ds_write_addtid_b32 %2 offset:%c8\n\t"
+      "ds_write_addtid_b32 %3 offset:%c9\n\t"
+      "ds_write_addtid_b32 %4 offset:%c10\n\t"
+      "ds_write_addtid_b32 %5 offset:%c11\n\t"
+      "ds_write_addtid_b32 %5 offset:%c12\n\t"
+      "ds_write_addtid_b32 %5 offset:%c13\n\t"
+      "ds_write_addtid_b32 %5 offset:%c14\n\t"
+      "ds_write_addtid_b32 %5 offset:%c15"
       :
-      : "v"(0u), "i"(kRecOff), "i"(kRecOff + 256), "i"(kRecOff + 512), "i"(kRecOff + 768),
-        "i"(kRecOff + 1024)
+      : "v"(e[0]), "v"(e[1]), "v"(e[2]), "v"(e[3]), "v"(e[4]), "v"(0u),
+        "i"(kBufBytes), "i"(kBufBytes + 256), "i"(kBufBytes + 512), "i"(kBufBytes + 768),
+        "i"(kBufBytes + 1024), "i"(kRecOff), "i"(kRecOff + 256), "i"(kRecOff + 512),
+        "i"(kRecOff + 768), "i"(kRecOff + 1024)
       : "memory");
+}
+
+// key[64 r + lane] = k[r] over the walker queue (kQOff), one m0 set.
+__device__ __forceinline__ void keys_store_addtid(const uint32_t (&k)[5]) {
+  asm volatile(
+      "s_mov_b32 m0, 0\n\t"
+      "s_nop 0\n\t"
+      "ds_write_addtid_b32 %0 offset:%c5\n\t"
+      "ds_write_addtid_b32 %1 offset:%c6\n\t"
+      "ds_write_addtid_b32 %2 offset:%c7\n\t"
+      "ds_write_addtid_b32 %3 offset:%c8\n\t"
+      "ds_write_addtid_b32 %4 offset:%c9"
+      :
+      : "v"(k[0]), "v"(k[1]), "v"(k[2]), "v"(k[3]), "v"(k[4]), "i"(kQOff), "i"(kQOff + 256),
+        "i"(kQOff + 512), "i"(kQOff + 768), "i"(kQOff + 1024)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {   // v_ffbl_b32: -1 when x == 0
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
 }
 
 // Longest common prefix of the byte runs at a and b (a < b), capped at
@@ -236,31 +254,52 @@ __device__ __forceinline__ void rec_zero_addtid() {
 // VALU per block and lost).  Reads past the region land in its pad (>= 48 B
 // past any block end; the aligned form reads at most 19 past it).
 __device__ __forceinline__ int lcp(const uint8_t *d, int a, int b, int limit) {
+  // a step continues only after 16 equal bytes, so both operands keep their
+  // byte alignment: the shifts are loop-invariant and the dword pointers
+  // advance by 16 bytes
+  const uint32_t sa = (uint32_t)a & 3u, sb = (uint32_t)b & 3u;
+  const uint32_t *wa = reinterpret_cast<const uint32_t *>(d + (a & ~3));
+  const uint32_t *wb = reinterpret_cast<const uint32_t *>(d + (b & ~3));
   int l = 0;
-  bool diff;
-  do {                                    // 16 bytes per step, one exit condition
-    // 16 bytes at byte offset x from five aligned dwords (two ds_read2_b32 and
-    // a ds_read_b32: no misaligned replay), byte-aligned by v_alignbyte
-    auto at16 = [&](int x) {
-      const uint32_t *w = reinterpret_cast<const uint32_t *>(d + (x & ~3));
+  for (;;) {                              // 16 bytes per step
+    // 16 bytes from five aligned dwords (two ds_read2_b32 and a ds_read_b32:
+    // no misaligned replay), byte-aligned by v_alignbyte
+    auto at16 = [](const uint32_t *w, uint32_t sh) {
       const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-      const uint32_t sh = (uint32_t)(x & 3);
       return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh),
                         __builtin_amdgcn_alignbyte(w2, w1, sh),
                         __builtin_amdgcn_alignbyte(w3, w2, sh),
                         __builtin_amdgcn_alignbyte(w4, w3, sh));
     };
-    const uint4 A = at16(a + l), B = at16(b + l);
-    const uint64_t x0 = ((uint64_t)(A.y ^ B.y) << 32) | (A.x ^ B.x);
-    const uint64_t x1 = ((uint64_t)(A.w ^ B.w) << 32) | (A.z ^ B.z);
-    diff = (x0 | x1) != 0;
-    // first differing byte, branch-free (a select, not an exec-masked if/else)
-    const uint32_t a0 = (uint32_t)__builtin_ctzll(x0 | (1ull << 63)) >> 3;
-    const uint32_t a1 = 8u + ((uint32_t)__builtin_ctzll(x1 | (1ull << 63)) >> 3);
-    const uint32_t m0 = 0u - (uint32_t)(x0 != 0);
-    const uint32_t at = (a0 & m0) | (a1 & ~m0);
-    l += diff ? (int)at : 16;
-  } while (!diff && l < limit);
+    const uint4 A = at16(wa, sa), B = at16(wb, sb);
+    // first differing bit of the 16 bytes: v_ffbl per dword (-1 when equal),
+    // offset by 32 k with an OR (each is < 32 or all ones), min over the four
+    const uint32_t m = min(min(ffbl(A.x ^ B.x), ffbl(A.y ^ B.y) | 32u),
+                           min(ffbl(A.z ^ B.z) | 64u, ffbl(A.w ^ B.w) | 96u));
+    l += (int)min(m >> 3, 16u);
+    if (m != 0xFFFFFFFFu || l >= limit) break;
+    wa += 4;
+    wb += 4;
+  }
+  return l < limit ? l : limit;
+}
+
+// The same over the 4-gram keys (kj = &key[j], kp = &key[p], j < p): the
+// 16 bytes at a position are key[x], key[x + 4], key[x + 8], key[x + 12].
+// key[] covers positions 0 .. 319 and a step reads at most 12 past p + l
+// < n <= 300.
+__device__ __forceinline__ int lcp_keys(const uint32_t *kj, const uint32_t *kp, int limit) {
+  int l = 0;
+  for (;;) {
+    const uint32_t a0 = kj[0], a1 = kj[4], a2 = kj[8], a3 = kj[12];
+    const uint32_t b0 = kp[0], b1 = kp[4], b2 = kp[8], b3 = kp[12];
+    const uint32_t m = min(min(ffbl(a0 ^ b0), ffbl(a1 ^ b1) | 32u),
+                           min(ffbl(a2 ^ b2) | 64u, ffbl(a3 ^ b3) | 96u));
+    l += (int)min(m >> 3, 16u);
+    if (m != 0xFFFFFFFFu || l >= limit) break;
+    kj += 16;
+    kp += 16;
+  }
   return l < limit ? l : limit;
 }
 
@@ -337,136 +376,135 @@ __device__ __forceinline__ void wave_sync() {
 // recs (global: the block's slot); returns the bytes its stream takes.
 // kMatchesOnly: stop after the best-match scan and store every position's
 // find_longest_match result to mout instead (lz4r_block_matches_device).
-template <bool kMatchesOnly>
-__device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restrict__ mout,
+template <bool kMatchesOnly, bool kFull>
+__device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__restrict__ mout,
                                             uint32_t *__restrict__ recs) {
+  // kFull: a whole 300-byte block (every block but possibly the last): n is
+  // a constant and only round 4's lanes 41..63 hold positions past the last
+  // 4-gram start
+  const int n = kFull ? kBlk : n_arg;
   const int lane = threadIdx.x;
   constexpr int base = kInOff;
 
   // ---- index: per-bucket chains of the 4-gram starts -----------------------
-  // Position p exchanges itself (as the byte offset 4 p) into its bucket's
-  // u32 head (kNoLink = empty) and keeps the previous head as its link.  The
-  // chains are in insertion order: rounds ascend, and lanes of one round that
-  // share a bucket are chained in the order the LDS served their exchanges.
-  // Entry: link (11 bits) | 5-bit tag << 17 | preceding byte (9 bits) << 22.
-  // Every unordered pair of a bucket is met once, by the later-inserted of
-  // the two walking its chain; a lane keeps its walker until the chain ends,
-  // so each pass is balanced over the lanes whatever the chain lengths.
+  // Position-major: lane l owns p_r = 64 r + l (r = 0..4; positions 297..319
+  // of a full block start no 4-gram).  Round r exchanges the 64 positions
+  // 64 r .. 64 r + 63 into their buckets' u32 heads (ds_wrxchg_rtn_b32, the
+  // five rounds back to back, one wait) and keeps each old head as the
+  // position's link.  Insertion is in ascending position order (rounds
+  // ascend; within one exchange the LDS serves the lanes in ascending order),
+  // so every link is a smaller byte offset than its position or kNoLink: a
+  // chain strictly decreases, and a walk that stops at the first link not
+  // below the current one ends on any input -- even on a corrupted head.
+  // Entry (byte offsets 4 p):  link (bits 0..10) | p == 0 (bit 15) |
+  // preceding byte (16..23) | tag (24..31, hash bits 16..23; within a bucket
+  // only bits 16..21 can differ).  Entries are written by ds_write_addtid_b32
+  // (2 LDS cycles per round instead of 4-6 for a strided store).
   PROF_DECL;
   const bool search = LZ4R_VARIANT != 1 && LZ4R_VARIANT != 2;
   const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
-  // 1024 u32 heads (4 KB) overlay the queue, the candidates and the front of
-  // ent and rec -- all dead until the heads are (ent and rec are written
-  // after the exchanges)
-  head_reset_addtid();                   // empty heads (the previous block's data)
-  // Blocked layout: lane l owns the five positions p0 .. p0 + 4, p0 = 5 l
-  // (lanes 60..63 own none of a 300-B block).  One 12-byte window per lane
-  // gives all five 4-gram keys and preceding bytes; the five head swaps go
-  // out back to back.  Chain order need not follow position order: a pair is
-  // met once whichever of the two was inserted later, and is ordered by
-  // position when it is used.
-  const int p0 = 5 * lane;
-  uint32_t item[5];
+
+  bool walk[5];                          // p_r has a link (a walker)
+  uint32_t key[5];                       // p_r's 4-gram (kept for the lcp drain)
   {
-    // bytes p0 - 1 .. p0 + 10 (lane 0's byte -1 unused) from four aligned dwords
-    const int wb = base + p0 - 1;
-    const uint32_t *wd = reinterpret_cast<const uint32_t *>(S.buf) + (wb >> 2);
-    const uint32_t a0 = wd[0], a1 = wd[1], a2 = wd[2], a3 = wd[3];
-    const uint32_t wsh = (uint32_t)(wb & 3);
-    const uint32_t d0 = __builtin_amdgcn_alignbyte(a1, a0, wsh);
-    const uint32_t d1 = __builtin_amdgcn_alignbyte(a2, a1, wsh);
-    const uint32_t d2 = __builtin_amdgcn_alignbyte(a3, a2, wsh);
-    const uint32_t key[5] = {__builtin_amdgcn_alignbyte(d1, d0, 1u),
-                             __builtin_amdgcn_alignbyte(d1, d0, 2u),
-                             __builtin_amdgcn_alignbyte(d1, d0, 3u), d1,
-                             __builtin_amdgcn_alignbyte(d2, d1, 1u)};
-    uint32_t adr[5], set[5], hv[5];
-    // inactive positions exchange with a dword of rec[192..320), past the
-    // heads and zeroed after the exchanges (distinct addresses per lane)
-    const uint32_t dummy = (uint32_t)(kRecOff + 4 * (192 + 5 * (lane & 15)) - kHeadOff);
+    // bytes p .. p + 3 from two aligned dwords: sh = p & 3 = lane & 3
+    const uint32_t sh = (uint32_t)lane & 3u;
+    const uint32_t *bw = reinterpret_cast<const uint32_t *>(S.buf) + (kInOff >> 2) + (lane >> 2);
+    uint32_t pt[5], adr[5], set[5];
+    // inactive positions (p >= nk) exchange with a dword of rec[192 + lane]
+    // (past the heads, zeroed after the exchanges; distinct per lane)
+    const uint32_t dummy = (uint32_t)(kRecOff + 4 * (192 + lane) - kHeadOff);
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-      const int p = p0 + r;
-      const bool act = search && p < nk;
-      hv[r] = key[r] * 2654435761u;             // bucket = top 10 bits, tag = the next 5
-      adr[r] = act ? (hv[r] >> (32 - kHB)) << 2 : dummy + 4u * (uint32_t)r;
-      set[r] = (uint32_t)(4 * p);               // heads hold byte offsets 4 p
+      const uint32_t w1 = bw[16 * r], w2 = bw[16 * r + 1];          // one ds_read2_b32
+      key[r] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+      // blk[p - 1] = byte 0 of key(p - 1): the lane below's key (DPP
+      // wave_shr:1), for lane 0 lane 63's key of the round before (round 0's
+      // lane 0 is p = 0, whose byte is the sentinel bit below)
+      const uint32_t below = r ? (uint32_t)__builtin_amdgcn_readlane((int)key[r - 1], 63) : 0u;
+      const uint32_t pb = (uint32_t)__builtin_amdgcn_update_dpp((int)below, (int)key[r], 0x138,
+                                                               0xf, 0xf, false);
+      const uint32_t hv = key[r] * 2654435761u;                    // bucket = top 10 bits
+      // [0, 0, blk[p - 1], hash bits 16..23]: the entry without its link
+      pt[r] = __builtin_amdgcn_perm(pb, hv, 0x02040C0Cu);
+      const int p = 64 * r + lane;
+      // (full block: rounds 0..3 are all 4-gram starts)
+      const bool act = search && ((kFull && r < 4) || p < nk);
+      adr[r] = act ? (hv >> (32 - kHB)) << 2 : dummy;
+      set[r] = (uint32_t)(4 * p);
     }
+    if (lane == 0) pt[0] |= 1u << 15;     // p = 0: left-maximal with every later position
     uint32_t old[5];
     xchg_rtn5(old, adr, set);
-    rec_zero_addtid();                   // local(p) accumulators (past n: unused)
+    uint32_t e[5];
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-      const int p = p0 + r;
-      // the previous head: a byte link (kNoLink: none)
-      const uint32_t link = old[r];
-      // blk[p - 1]; 256 for p = 0, which so differs from every byte and makes
-      // every pair with j = 0 left-maximal
-      uint32_t pb = r < 4 ? (d0 >> (8 * r)) & 255u : d1 & 255u;
-      if (r == 0) pb |= lane == 0 ? 256u : 0u;
-      const bool act = search && p < nk;
-      // within a bucket only the tag's low 5 bits can differ
-      S.ent[p] = link | (hv[r] & (31u << 17)) | (pb << 22);   // inactive: never read
-      item[r] = act && link != kNoLink ? (uint32_t)(4 * p) | (link << 16) : 0u;
+      e[r] = old[r] | pt[r];             // inactive: never read (no chain reaches it)
+      walk[r] = (int)old[r] < 4 * (64 * r + lane);   // kNoLink (2044) > every 4 p
     }
+    ent_store_rec_zero_addtid(e);        // ent[64 r + lane] = e[r]; rec[] = 0
   }
   PROF_MARK(0);                       // index
   wave_sync();                       // the heads are dead: the queue overlays them
-  // queue the walkers lane-major: one wave scan of the per-lane counts
-  int qwr;                               // walkers queued (S.q()[0 .. qwr))
-  {
-    int cnt = 0;
+  // queue the walkers row by row from r = 4 down (later positions first: the
+  // deepest chains start early, which keeps the walk passes near the
+  // longest chain), lanes ascending within a row
+  uint32_t qend = kQOff;                 // byte offset past the last queued walker
 #pragma unroll
-    for (int r = 0; r < 5; ++r) cnt += item[r] != 0u;   // p != link: a walker's item is never 0
-    const uint32_t inc = wave_incl_add((uint32_t)cnt);
-    qwr = (int)__builtin_amdgcn_readlane((int)inc, 63);
-    int at = (int)inc - cnt;
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const bool walk = item[r] != 0u;
-      // branch-free: lanes without a walker write their own dword of the idle cand list
-      *(walk ? &S.q()[at] : &S.cand()[lane]) = item[r];
-      at += walk;
-    }
+  for (int r = 4; r >= 0; --r) {
+    const uint64_t m = ballot(walk[r]);
+    // branch-free: a lane without a walker writes its own dword of the idle
+    // candidate list (the select reads the mask straight from SGPRs)
+    const uint32_t at = sel_mask(m, ((uint32_t)rank_below(m) << 2) + qend,
+                                 (uint32_t)(kCandOff + 4 * lane));
+    *reinterpret_cast<uint32_t *>(S.buf + at) = (uint32_t)(4 * (64 * r + lane));
+    qend += 4u * (uint32_t)__popcll(m);
   }
+  const int qwr = (int)(qend - kQOff) >> 2;   // walkers queued (S.q()[0 .. qwr))
   wave_sync();
 
   PROF_MARK(1);                       // walker queue
   // ---- candidates: walk the chains ------------------------------------------
   // A pair (j < p) of one bucket is a candidate when the tags agree and the
-  // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]).  Walkers, links
-  // and candidates carry byte offsets 4 p into the entry arrays (no shifts
-  // per pass); entry = link | tag << 17 | prev byte << 22 (256 at p = 0).
-  // Candidates go to
-  // a list in S.cand, drained by a balanced lcp pass with LDS atomicMax into
-  // S.rec ((p + len) << 9 | (p - j): the longest, ties to the smallest j).
+  // match is left-maximal (j == 0 or blk[j-1] != blk[p-1]): with x = the two
+  // entries xor'ed, exactly when 2^15 <= x < 2^24 (bits 24..31 zero: the
+  // tags agree; some bit 15..23 set: the preceding bytes differ or j == 0).
+  // Candidates go to a list in S.cand, drained by a balanced lcp pass with
+  // LDS atomicMax into S.rec ((p + len) << 9 | (p - j): the longest, ties to
+  // the smallest j).
   if (search && LZ4R_VARIANT != 3) {
     constexpr int kTrash = kCand - 1;
     int ncand = 0;
     const uint8_t *const entb = reinterpret_cast<const uint8_t *>(S.ent);
     auto ent_at = [&](int off) { return *reinterpret_cast<const uint32_t *>(entb + off); };
-    auto drain = [&]() {
+    // kKeys: the walk is over and the queue region holds every position's
+    // 4-gram key (key[p] = bytes p .. p + 3 as a dword), so a 16-byte lcp
+    // step is four aligned dword reads per operand (two ds_read2_b32), with
+    // no byte alignment; a drain in the middle of the walk (more than 63
+    // candidates) reads the staged block with v_alignbyte
+    auto drain = [&](auto keys) {
+      constexpr bool kKeys = decltype(keys)::value;
       wave_sync();
       for (int i = lane; i < ncand && LZ4R_VARIANT != 4; i += 64) {
         const uint32_t pr = S.cand()[i];
-        const int ea = (int)(pr & 0xFFFFu) >> 2, eb = (int)(pr >> 18);
-        const int p = max(ea, eb), j = min(ea, eb);
-        const int l = lcp(S.buf, base + j, base + p, n - p);
+        const int p = (int)(pr & 0xFFFFu) >> 2, j = (int)(pr >> 18);   // j < p: chains decrease
+        const int l = kKeys ? lcp_keys(S.q() + j, S.q() + p, n - p)
+                            : lcp(S.buf, base + j, base + p, n - p);
         // (end, dist) as the best scan wants it: for one p the larger end is
         // the longer match and the larger dist the smaller source
-        if (l >= 4) atomicMax(&S.rec[p], ((uint32_t)(p + l) << 9) | (uint32_t)(p - j));
+        if (LZ4R_VARIANT == 5) {          // ablation: the lcp without its result
+          if (l == 12345) S.rec[0] = 1u;
+        } else if (l >= 4) {
+          atomicMax(&S.rec[p], ((uint32_t)(p + l) << 9) | (uint32_t)(p - j));
+        }
       }
       wave_sync();
     };
     // Persistent walkers: a lane keeps its walker (a walks, b = the next chain
     // entry) in registers until the chain ends, and an idle lane takes the
     // next queued walker.  The queue is read once, front to back: no ring,
-    // no re-queue stores.
-    // The walkers' liveness is kept as a scalar lane mask: a ballot of a
-    // loop-carried bool costs two VALU (v_cndmask + v_cmp) per use, and the
-    // selects take the mask straight from SGPRs (every mask here is last
-    // written by a SALU op: no VALU-SGPR hazard)
-    // queue and candidate positions as byte offsets (4 i): one v_lshl_add each
+    // no re-queue stores.  The walkers' liveness is a scalar lane mask (the
+    // selects read it straight from SGPRs, written by SALU ops only).
     int qrd4 = 0;
     const int qwr4 = 4 * qwr;
     const uint8_t *const qb = reinterpret_cast<const uint8_t *>(S.q());
@@ -474,40 +512,51 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     int a = 0, b = 0;
     uint32_t me = 0;                       // the walker's own entry (re-read only on a take)
     uint64_t vm = 0;                       // lanes holding a walker
-    for (;;) {
-      if (qrd4 < qwr4) {                   // (uniform) idle lanes take queued walkers
-        const uint64_t em = ~vm;
-        const int idx4 = qrd4 + (rank_below(em) << 2);
-        const uint64_t nm_ = em & ballot(idx4 < qwr4);
-        const uint32_t it = *reinterpret_cast<const uint32_t *>(qb + idx4);   // idx <= qwr + 63 < kQ
-        a = (int)sel_mask(nm_, it & 0xFFFFu, (uint32_t)a);
-        b = (int)sel_mask(nm_, it >> 16, (uint32_t)b);
-        vm |= nm_;
-        qrd4 += 4 * __popcll(em);
-        me = ent_at(a);                    // (lanes that kept their walker read the same word)
-      }
-      if (vm == 0) break;                  // no walker left and the queue is empty
+    // one pass: every live walker meets its next chain entry
+    auto pass = [&]() {
       const uint32_t o = ent_at(b);
-      const uint32_t x = me ^ o;
-      // a ballot of each compare (a ballot of a combined bool costs two VALU)
-      const uint64_t cm = vm & ballot((x & (31u << 17)) == 0) & ballot(x >= (1u << 22));
+      const uint64_t cm = vm & ballot(((me ^ o) - (1u << 15)) < (1u << 24) - (1u << 15));
       const int sl4 =
           (int)sel_mask(cm, (uint32_t)(4 * ncand + (rank_below(cm) << 2)), (uint32_t)(4 * kTrash));
-      // the pair as walked (walker, chain entry): the drain orders it
+      // the pair (walker, chain entry): the entry is the earlier position
       *reinterpret_cast<uint32_t *>(cb + sl4) = (uint32_t)a | ((uint32_t)b << 16);
       ncand += __popcll(cm);
-      b = (int)(o & 2047u);
-      vm &= ballot(b != (int)kNoLink);
-      if (ncand > kTrash - 64) {
-        drain();
+      const int bn = (int)(o & 2047u);
+      vm &= ballot(bn < b);                // the chain ends (kNoLink, or any non-decreasing link)
+      b = bn;
+      if (ncand > kTrash - 64) {           // (rare: a full list drains mid-walk)
+        drain(std::false_type{});
         ncand = 0;
       }
+    };
+    // while walkers are queued, idle lanes take them (uniform); then the
+    // passes go on without the take
+    while (qrd4 < qwr4) {
+      const uint64_t em = ~vm;
+      const int idx4 = qrd4 + (rank_below(em) << 2);
+      const uint64_t nm_ = em & ballot(idx4 < qwr4);
+      const uint32_t it = *reinterpret_cast<const uint32_t *>(qb + idx4);   // idx <= qwr + 63 < kQ
+      a = (int)sel_mask(nm_, it, (uint32_t)a);
+      vm |= nm_;
+      qrd4 += 4 * __popcll(em);
+      me = ent_at(a);                      // (lanes that kept their walker read the same word)
+      b = (int)sel_mask(nm_, me & 2047u, (uint32_t)b);   // a new walker starts at its link
+      pass();
     }
-    if (ncand) drain();
+    while (vm) pass();
+    if (ncand) {
+      keys_store_addtid(key);            // the queue is dead: keys over it
+      drain(std::true_type{});
+    }
   }
   wave_sync();
   PROF_MARK(2);                       // candidates + lcp
   // ---- best(p) = prefix lexmax of (end, dist) -------------------------------
+  // (from here on the per-position phases are BLOCKED: lane l owns
+  // p = 5 l .. 5 l + 4, so a prefix over positions is a running max over the
+  // lane's five plus one wave scan; the arrays in LDS are indexed by p in
+  // either layout)
+  const int p0 = 5 * lane;
   // blocked: a running max over the lane's five positions, one wave scan of
   // the lane totals, the exclusive prefix folded back in
   uint32_t v[5];
@@ -536,7 +585,11 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   }
   // x = v - p << 9 = len << 9 | dist (len <= 0, i.e. x < 512 or negative,
   // where no match covers p); the record's low 17 bits are dist | M << 9 with
-  // M = len & 0xFF for len >= 4 (the uint8_t return, LZ4.c:317), else 0
+  // M = len & 0xFF (the uint8_t return, LZ4.c:317).  A match starts at p when
+  // len >= 4 and M != 0 (len 256 is a literal, LZ4.c:521); elsewhere the
+  // word's M and dist are 0 (the succ gather below then reads nm[p]: the
+  // lanes' stride-5 words, conflict-free; the lanes past the last match
+  // sequence read M = dist = 0 at rec[n]).
   uint32_t mrec[5];
   bool mt[5];                     // a match starts at p (M != 0)
   int f[6];                       // f[r] = 4 x the first matchable position >= p0 + r
@@ -544,8 +597,9 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
     const uint32_t x = v[r] - P9 - ((uint32_t)r << 9);
-    mrec[r] = x & ((int)x >= (4 << 9) ? 0x1FFFFu : 0x1FFu);
-    mt[r] = mrec[r] >= 512u;
+    const uint32_t w = x & 0x1FFFFu;
+    mt[r] = (int)x >= (4 << 9) && w >= 512u;
+    mrec[r] = mt[r] ? w : 0u;
   }
 
   PROF_MARK(3);                       // best scan
@@ -559,7 +613,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
     const uint64_t has = ballot(loc < (1 << 20));
     const uint64_t up = has & ~((2ull << lane) - 1ull);  // lanes above this one
     const int src = up ? ctz64(up) : lane;
-    const int nx = __shfl(loc, src, 64);
+    const int nx = __builtin_amdgcn_ds_bpermute(src << 2, loc);   // src in 0..63
     f[5] = up ? nx : 4 * n;
 #pragma unroll
     for (int r = 4; r >= 0; --r) f[r] = mt[r] ? 4 * (p0 + r) : f[r + 1];
@@ -570,12 +624,23 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   wave_sync();
   // succ(p) = nm(p + M(p)) for the match starts, kept in the record word:
   // rec[p] = dist | M << 9 | 4 succ << 17 (branch-free: the words of
-  // positions that start no match are written too and never read)
+  // positions that start no match are written too, with M = dist = 0)
+  {
+    const uint32_t p4 = 4u * (uint32_t)p0;
+    uint32_t sj[5];
 #pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int q = p0 + r;
-    const int sj = (int)S.nm[q + (int)(mrec[r] >> 9)];   // q + M <= n: matches end in the block
-    S.rec[q] = mrec[r] | ((uint32_t)sj << 17);
+    for (int r = 0; r < 5; ++r) {
+      // nm[q + M], q = p0 + r (q + M <= n: matches end in the block); the
+      // byte address by v_bfe + v_lshl_add (the compiler's shift-and-mask
+      // form takes three); the five gathers go out before any store
+      uint32_t a;
+      asm("v_bfe_u32 %0, %1, 9, 8\n\tv_lshl_add_u32 %0, %0, 2, %2"
+          : "=&v"(a) : "v"(mrec[r]), "v"(p4));
+      sj[r] = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(S.nm) + a +
+                                                  4 * r);
+    }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) S.rec[p0 + r] = mrec[r] | (sj[r] << 17);
   }
   const int F0 = __builtin_amdgcn_readlane(f[0], 0);    // nm(0)
   wave_sync();
@@ -647,49 +712,54 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n, uint32_t *__restr
   int ocar = 3;                      // block header: u8 nseq, u16 size
   int szsum = 0;
   int end_prev = 0;                  // end of the previous round's last match
-  for (int s0 = 0; LZ4R_VARIANT != 11; s0 += 64) {
-    const int kk = s0 + lane;
-    uint32_t cq;
-    if (!slow) {
-      cq = kk < it ? seqv >> 19 : (uint32_t)n;                    // (kk < it only in round 0)
-    } else {
-      cq = kk < Sv_slow ? S.seq()[kk] : (uint32_t)n;
-    }
+  // one round: sequence kk = s0 + lane starts its match at cq (n past the
+  // matches); returns false once the round holds the last sequence
+  auto round = [&](int kk, uint32_t cq) {
     const bool ism = (int)cq < n;                                  // ends with a match
-    const uint64_t mm = ballot(ism);
-    const int nm_r = __popcll(mm);                                 // a prefix of the round
-    const uint32_t rv = S.rec[cq];        // cq <= n
-    const int cpos = ism ? (int)cq : n;
-    const int M = ism ? (int)((rv >> 9) & 255u) : 0;
-    const int D = ism ? (int)(rv & 511u) : 0;                     // the tail writes offset 0
-    const int end = cpos + M;
+    const int nm_r = __popcll(ballot(ism));                        // a prefix of the round
+    const uint32_t rv = S.rec[cq];        // cq <= n; M = D = 0 at rec[n]: past the matches
+    const int M = (int)((rv >> 9) & 255u);
+    const int end = (int)cq + M;
     const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
     const int pend = lane == 0 ? end_prev : (int)upv;             // literal run start
     end_prev = (int)lane63((uint32_t)end);
-    const int L = cpos - pend;
-    const bool act = ism || (lane == nm_r && pend < n);            // the tail: literals left
-    // bytes written (LZ4.c:365-413) and the size field (LZ4.c:546-575), which
-    // differ for M = 1..3: the field counts a match-extension byte that
-    // write_sequence never writes
-    const int rem = (L - 15) & 255;
-    const int le = L >= 15 ? (rem == 255 ? 2 : 1) : 0;             // literal-extension bytes
-    const int mx = (M - 4) & 255;
-    const bool mextW = M >= 4 && mx >= 15, mextS = M != 0 && mx >= 15;
-    const uint32_t ws = act ? (uint32_t)(5 + le + L) * 0x10001u + (mextW ? 1u : 0u) +
-                                  (mextS ? 0x10000u : 0u)
-                            : 0u;
-    const uint32_t tot = lane63(wave_incl_add(ws));
-    if (act) recs[1 + kk] = (uint32_t)cpos | ((uint32_t)M << 9) | ((uint32_t)D << 17);
+    const int L = (int)cq - pend;
+    // + the tail (lane nm_r, when literals are left); the mask from ballots
+    // of the compares (a ballot of a combined bool costs two VALU)
+    const uint64_t am = ballot(ism) | (ballot(lane == nm_r) & ballot(pend < n));
+    // bytes written (LZ4.c:365-413) | the size field (LZ4.c:546-575) << 16:
+    // 5 + L + the literal-extension bytes (one from 15, two at L = 270, where
+    // the uint8_t remainder is 255: LZ4.c:376-385) + a match-extension byte
+    // (M >= 19); the size field also counts one for M = 1..3, which
+    // write_sequence never writes (LZ4.c:393 vs :562-575)
+    uint32_t ws = (uint32_t)(L + 5 + (L >= 15 ? 1 : 0) + (L == 270 ? 1 : 0)) * 0x10001u;
+    ws += M >= 19 ? 0x10001u : 0u;
+    ws += (uint32_t)(M - 1) < 3u ? 0x10000u : 0u;
+    const uint32_t tot = lane63(wave_incl_add(sel_mask(am, ws, 0u)));
+    if (sel_mask(am, 1u, 0u))
+      recs[1 + kk] = cq | (rv & 0x1FE00u) | ((rv & 511u) << 17);   // start | M | dist
     ocar += (int)(tot & 0xFFFFu);
     szsum += (int)(tot >> 16);
-    nseq += (int)__popcll(ballot(act));
-    if (nm_r < 64) break;
+    nseq += (int)__popcll(am);
+    return nm_r == 64;
+  };
+  if (LZ4R_VARIANT != 11) {
+    // round 0 from the walk's register; more than 64 sequences (the walk's
+    // register wrapped) come from the redone walk in S.seq
+    const uint32_t c0 = slow ? S.seq()[lane] : (lane < it ? seqv >> 19 : (uint32_t)n);
+    if (round(lane, c0)) {             // 64 match sequences: the tail or more follow
+      for (int s0 = 64;; s0 += 64) {
+        const int kk = s0 + lane;
+        if (!round(kk, slow && kk < Sv_slow ? S.seq()[kk] : (uint32_t)n)) break;
+      }
+    }
   }
   PROF_MARK(6);                       // records
   if (lane == 0) recs[0] = (uint32_t)szsum | ((uint32_t)nseq << 16);
   return ocar;
 }
 
+template <bool kAligned>   // the input is 4-byte aligned (the host checks)
 __global__ __launch_bounds__(64) void lz4_tiles(
     const uint8_t *__restrict__ in, uint32_t nb, uint32_t per, uint32_t last_n,
     uint8_t *__restrict__ slots, uint32_t *__restrict__ usz, uint16_t *__restrict__ bsizes) {
@@ -707,12 +777,16 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   // ---- stage the block: 75 dwords, both loads in flight; 16-B zero pad ------
   {
     uint32_t *dst = reinterpret_cast<uint32_t *>(S.buf + kInOff);
-    if (n == kBlk && ((uintptr_t)in & 3) == 0) {
+    if (kAligned && n == kBlk) {
+      // branch-free: the second load's address is clamped to the block's
+      // last dword, lanes 11.. store zeros -- the 48-B pad past the block
+      // and, for lanes 23.., dwords under the bucket heads, which are emptied
+      // after this
       const uint32_t *q = reinterpret_cast<const uint32_t *>(src);
       const uint32_t v0 = q[lane];
-      const uint32_t v1 = lane < 11 ? q[64 + lane] : 0u;
+      const uint32_t v1 = q[64 + min(lane, 10)];
       dst[lane] = v0;
-      if (lane < 15) dst[64 + lane] = v1;
+      dst[64 + lane] = lane < 11 ? v1 : 0u;
     } else {
       for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
       if (lane < 16) S.buf[kInOff + n + lane] = 0;
@@ -720,8 +794,9 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   }
   wave_sync();
 
-  const int W = encode_block<false>(S, n, nullptr,
-                                   reinterpret_cast<uint32_t *>(slots + (size_t)t * kSlot));
+  uint32_t *const recs = reinterpret_cast<uint32_t *>(slots + (size_t)t * kSlot);
+  const int W = n == kBlk ? encode_block<false, true>(S, n, nullptr, recs)
+                          : encode_block<false, false>(S, n, nullptr, recs);
   if (lane == 0) {
     usz[t] = (uint32_t)W;
     bsizes[t] = (uint16_t)W;
@@ -741,7 +816,7 @@ __global__ __launch_bounds__(64) void lz4_matches(const uint8_t *__restrict__ in
   for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
   if (lane < 16) S.buf[kInOff + n + lane] = 0;
   wave_sync();
-  encode_block<true>(S, n, mout + (size_t)t * kBlk, nullptr);
+  encode_block<true, false>(S, n, mout + (size_t)t * kBlk, nullptr);
 }
 
 // find_longest_match over a block of any length n (block_encode with a
@@ -1206,8 +1281,13 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
     // slower also with the next block prefetched into registers)
     const uint32_t per = (uint32_t)((nbc + 7) / 8);    // blocks per XCD slice
     if (timed) (void)hipEventRecord(c->ev_tiles[2 * k], s);
-    hipLaunchKernelGGL(lz4_tiles, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk, (uint32_t)nbc,
-                       per, last_n, c->slots, c->tsz + b0, c->bsizes + b0);
+    // (every chunk starts 300 b0 bytes in: a multiple of 4)
+    if (((uintptr_t)in & 3) == 0)
+      hipLaunchKernelGGL(lz4_tiles<true>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
+                         (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0);
+    else
+      hipLaunchKernelGGL(lz4_tiles<false>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
+                         (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0);
     if (timed) (void)hipEventRecord(c->ev_tiles[2 * k + 1], s);
     const size_t p0 = b0 / kPart, np = (nbc + kPart - 1) / kPart;
     hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)np), dim3(256), 0, s, c->tsz, b1, p0,

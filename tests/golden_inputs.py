@@ -38,11 +38,28 @@ def _lit270():
     return u + u[:30] + _rng_bytes(12, 300)
 
 
+def _many_sequences(seed=3, nblocks=40):
+    """Blocks of a few dozen distinct bytes followed by random 4-byte chunks
+    of that prefix: the greedy parse takes many exact-4 matches with no
+    literals between them, and some blocks have more than 64 sequences
+    (the compressor's multi-round sequence path)."""
+    r = np.random.default_rng(seed)
+    out = bytearray()
+    for _ in range(nblocks):
+        pre = bytes(r.permutation(256)[:int(r.integers(10, 60))].astype(np.uint8))
+        rest = bytearray()
+        while len(pre) + len(rest) < 300:
+            s = int(r.integers(0, len(pre) - 4))
+            rest += pre[s:s + 4]
+        out += (pre + bytes(rest))[:300]
+    return bytes(out)
+
+
 LZ4_EDGE_CASES = [
     "exact_300", "exact_301", "exact_599", "exact_600", "a_x_600", "ab_x_700",
     "zeros_900", "random_bytes_3000", "alphabet2_3000", "alphabet4_3000",
     "m_eq_1", "m_eq_2", "m_eq_3", "len_256", "lit_270", "lit_300",
-    "text_last_block_1", "text_last_block_4", "text_10000",
+    "text_last_block_1", "text_last_block_4", "text_10000", "many_sequences",
 ]
 
 
@@ -76,5 +93,6 @@ def lz4_input(name):
         "text_last_block_1": lambda: text[5000:5601],
         "text_last_block_4": lambda: text[6000:6604],
         "text_10000": lambda: text[7000:17000],
+        "many_sequences": _many_sequences,
     }
     return table[name]()

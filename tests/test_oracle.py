@@ -100,3 +100,13 @@ def test_reconstruction_oracle_matches_reference(oracle, w, h, seed):
         pytest.skip("reference not built")
     got = oracle_api.reconstruct(oracle, oracle.rand_image(w, h, seed=seed))
     assert np.array_equal(got, ref)
+
+
+def test_many_sequences_input_covers_the_multi_round_path(oracle):
+    """The edge case 'many_sequences' holds blocks of 64 and of more than 64
+    sequences (the compressor's sequence rounds are 64 wide), checked here so
+    the GPU golden test keeps covering that path."""
+    import golden_inputs
+    d = golden_inputs.lz4_input("many_sequences")
+    counts = [oracle.lz4_blocks(d[300 * b:300 * b + 300], 0, 1)[0] for b in range(len(d) // 300)]
+    assert 64 in counts and max(counts) > 64
