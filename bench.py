@@ -39,13 +39,13 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TOPS = 39.3     # 78.6 TFLOPS fp64 vector spec counts FMA as 2
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # (tools/traffic.sh -> tools/traffic_summary.py, gfx950 FETCH correction applied)
-TRAFFIC_JSON = os.path.join(REPO, "profiles", "r02_traffic.json")
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r03_traffic.json")
 # per-launch instruction counts of lz4_tiles + measured SIMD issue rates
 # (tools/issue.sh -> tools/issue_summary.py)
-ISSUE_JSON = os.path.join(REPO, "profiles", "r02_issue.json")
+ISSUE_JSON = os.path.join(REPO, "profiles", "r03_issue.json")
 # clock each kernel holds under its own load (DVFS give-back), from a
 # GRBM_GUI_ACTIVE PMC pass (tools/clock_pmc.sh -> tools/clock_summary.py)
-CLOCK_JSON = os.path.join(REPO, "profiles", "r02_clock.json")
+CLOCK_JSON = os.path.join(REPO, "profiles", "r03_clock.json")
 SPEC_CLOCK_GHZ = 2.4
 
 CFG4_BYTES = 64 << 30          # configs[3]
@@ -58,17 +58,18 @@ def log(*a):
 
 
 def _profile_json(path):
-    """This round's profile, else the previous round's."""
-    if os.path.exists(path):
-        return path
-    old = path.replace("r02_", "r01_")
-    return old if os.path.exists(old) else path
+    """This round's profile, else the latest earlier round's."""
+    for r in ("r03_", "r02_", "r01_"):
+        p = path.replace("r03_", r)
+        if os.path.exists(p):
+            return p
+    return path
 
 
 def held_clock(key):
     """Median clock (GHz) the profiled kernel `key` held, or None."""
     try:
-        return float(json.load(open(CLOCK_JSON))[key]["ghz_median"])
+        return float(json.load(open(_profile_json(CLOCK_JSON)))[key]["ghz_median"])
     except (OSError, KeyError, ValueError, TypeError):
         return None
 
@@ -101,7 +102,9 @@ def issue_roof(bytes_now, launch_ms):
     # the micro-benchmark's rate was measured at the clock it held (valu_rate's
     # v_add body); per cycle, the kernel's own clock sets its peak
     clk = {}
-    fk, fb = held_clock("lz4:lz4_tiles"), held_clock("valu:void body<0>")
+    # (lz4_tiles is a template since round 3: its clock key names the instance)
+    fk = held_clock("lz4:void lz4_tiles<true>") or held_clock("lz4:lz4_tiles")
+    fb = held_clock("valu:void body<0>")
     fm = held_clock("valu:void body<3>")               # the 4 VALU + 4 SALU body
     if fk and fb:
         pk = peak_valu * fk / fb

@@ -180,6 +180,13 @@ int lz4r_decompress_stream(const uint8_t *in, size_t in_len, uint8_t *out, size_
 int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
                   size_t *out_len);
 
+/* Synchronise `stream` and report whether any compress call on ctx since the
+ * last check met a corrupt bucket head in lz4_tiles' LDS index (a head that is
+ * neither empty nor an earlier position of the block: never on a sound LDS;
+ * the walk ends anyway, chains strictly decrease).  LZ4R_ERR_CORRUPT (and the
+ * status is cleared) or LZ4R_OK.  lz4r_compress_device checks by itself. */
+int lz4r_check(lz4r_ctx *ctx, void *stream);
+
 /* Measurement: when enabled, every compress call records HIP events on its
  * own launch stream around the whole call and around each launch of the
  * compressor kernel lz4_tiles (one per 2^24-block chunk of the input).

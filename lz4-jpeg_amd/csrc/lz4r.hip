@@ -65,6 +65,7 @@
 // lz4_tiles; ~1 B of input + ~0.43 B of record heads read and ~1.03 B
 // written by lz4_emit (+14 B/block of sizes and offsets).
 #include <hip/hip_runtime.h>
+#include <limits.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -117,9 +118,12 @@ constexpr int kArr = 320;                // per-position arrays: every lane's fi
                                          // (p = 5 l + r <= 319) in range, no index clamps
 constexpr int kQ = kBlk + 64;            // walker queue: reads run up to 63 past the last
 constexpr int kCand = 128;               // candidate list (drained when a pass could fill it)
+constexpr uint32_t kEmptyHead = 0xFFFFFFFCu;   // an emptied bucket head; as an entry's
+                                              // 11-bit link field it reads kNoLink
 constexpr uint32_t kNoLink = 2044;       // chain end: an empty head (0x07FC), a dword-aligned
                                          // offset, so the reads past a chain's end stay aligned
 static_assert(kArr >= 64 * 5, "blocked positions of all 64 lanes");
+static_assert((kEmptyHead & 0x7FFu) == kNoLink && kNoLink >= 4 * kArr, "the chain-end link");
 
 // LDS of one wave (4,976 B: 32 waves per CU).  Byte offsets in TileLds::buf:
 //   [kInOff, +348)     the block (byte kInOff - 1 is read as blk[-1]) + an
@@ -171,7 +175,7 @@ static_assert(kRecOff + 4 * kArr <= 4976, "LDS of one wave");
 // offset field); the LDS serves one wave's operations in order, so a later
 // exchange of the same head sees the earlier.
 // Each head this block uses is first emptied by the positions that hash to
-// it (five ds_write_b32 of kNoLink, before any exchange; the LDS serves one
+// it (five ds_write_b32 of kEmptyHead, before any exchange; the LDS serves one
 // wave's operations in order): a head no position of the block maps to is
 // never read, so the other ~800 of the 1024 need no reset (5 scattered
 // stores instead of 16 ds_write_addtid_b32 over the whole 4 KB).
@@ -191,7 +195,7 @@ __device__ __forceinline__ void xchg_rtn5(uint32_t (&old)[5], const uint32_t (&a
       "s_waitcnt lgkmcnt(0)"
       : "=&v"(old[0]), "=&v"(old[1]), "=&v"(old[2]), "=&v"(old[3]), "=&v"(old[4])
       : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]),
-        "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(kNoLink)
+        "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(kEmptyHead)
       : "memory");
 }
 
@@ -354,6 +358,13 @@ __device__ __forceinline__ int rank_below(uint64_t m) {
 
 
 
+// acc + the set bits of m in the lanes below this one (the adds fold into
+// v_mbcnt's accumulator)
+__device__ __forceinline__ uint32_t rank_below_plus(uint64_t m, uint32_t acc) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, acc));
+}
+
 // per lane: t where the lane's bit of m is set, else f (v_cndmask with the
 // mask straight from an SGPR pair)
 __device__ __forceinline__ uint32_t sel_mask(uint64_t m, uint32_t t, uint32_t f) {
@@ -378,7 +389,8 @@ __device__ __forceinline__ void wave_sync() {
 // find_longest_match result to mout instead (lz4r_block_matches_device).
 template <bool kMatchesOnly, bool kFull>
 __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__restrict__ mout,
-                                            uint32_t *__restrict__ recs) {
+                                            uint32_t *__restrict__ recs,
+                                            uint32_t *__restrict__ status) {
   // kFull: a whole 300-byte block (every block but possibly the last): n is
   // a constant and only round 4's lanes 41..63 hold positions past the last
   // 4-gram start
@@ -393,7 +405,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
   // five rounds back to back, one wait) and keeps each old head as the
   // position's link.  Insertion is in ascending position order (rounds
   // ascend; within one exchange the LDS serves the lanes in ascending order),
-  // so every link is a smaller byte offset than its position or kNoLink: a
+  // so every link is a smaller byte offset than its position or empty: a
   // chain strictly decreases, and a walk that stops at the first link not
   // below the current one ends on any input -- even on a corrupted head.
   // Entry (byte offsets 4 p):  link (bits 0..10) | p == 0 (bit 15) |
@@ -405,6 +417,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
   const int nk = n >= 4 ? n - 3 : 0;     // positions that start a 4-gram
 
   bool walk[5];                          // p_r has a link (a walker)
+  uint32_t qn = 0;                       // walkers queued
   uint32_t key[5];                       // p_r's 4-gram (kept for the lcp drain)
   {
     // bytes p .. p + 3 from two aligned dwords: sh = p & 3 = lane & 3
@@ -436,31 +449,47 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
     if (lane == 0) pt[0] |= 1u << 15;     // p = 0: left-maximal with every later position
     uint32_t old[5];
     xchg_rtn5(old, adr, set);
+#if LZ4R_VARIANT == 20
+    // tools build: one stale head (a forward link, as a missed reset would
+    // leave) -- the walk must still end and the call report LZ4R_ERR_CORRUPT
+    if (lane == 7) old[2] = 4u * 250u;
+#endif
     uint32_t e[5];
+    int d[5];
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-      e[r] = old[r] | pt[r];             // inactive: never read (no chain reaches it)
-      walk[r] = (int)old[r] < 4 * (64 * r + lane);   // kNoLink (2044) > every 4 p
+      // the link field is 11 bits: kEmptyHead reads kNoLink (2044)
+      e[r] = (old[r] & 0x7FFu) | pt[r];  // inactive: never read (no chain reaches it)
+      // a link (not an empty head, -4 as an int); on a sound LDS an earlier
+      // position -- checked below, and a walk ends at any non-decreasing link
+      walk[r] = (int)old[r] >= 0;
+      // a link is an earlier position (old - 4 p < 0) or an empty head
+      // (kEmptyHead = -4 as an int: old - 4 p < 0 too); anything else is a
+      // corrupt head.  One subtraction per position and two v_max3.
+      d[r] = (int)(old[r] - set[r]);
+    }
+    const int y = max(max(max(d[0], d[1]), d[2]), max(d[3], d[4]));
+    // (never on a sound LDS; the batch match finder has no status word)
+    if (!kMatchesOnly && ballot(y >= 0)) atomicOr(status, 1u);
+    // queue the walkers row by row from r = 4 down (later positions first:
+    // the deepest chains start early, which keeps the walk passes near the
+    // longest chain), lanes ascending within a row; the queue overlays the
+    // heads, dead after the exchanges (the LDS serves the wave in order)
+#pragma unroll
+    for (int r = 4; r >= 0; --r) {
+      const uint64_t m = ballot(walk[r]);
+      // branch-free: a lane without a walker writes its own dword of the idle
+      // candidate list (the select reads the mask straight from SGPRs)
+      const uint32_t at = sel_mask(m, (rank_below_plus(m, qn) << 2) + kQOff,
+                                   (uint32_t)(kCandOff + 4 * lane));
+      *reinterpret_cast<uint32_t *>(S.buf + at) = set[r];
+      qn += (uint32_t)__popcll(m);
     }
     ent_store_rec_zero_addtid(e);        // ent[64 r + lane] = e[r]; rec[] = 0
   }
-  PROF_MARK(0);                       // index
-  wave_sync();                       // the heads are dead: the queue overlays them
-  // queue the walkers row by row from r = 4 down (later positions first: the
-  // deepest chains start early, which keeps the walk passes near the
-  // longest chain), lanes ascending within a row
-  uint32_t qend = kQOff;                 // byte offset past the last queued walker
-#pragma unroll
-  for (int r = 4; r >= 0; --r) {
-    const uint64_t m = ballot(walk[r]);
-    // branch-free: a lane without a walker writes its own dword of the idle
-    // candidate list (the select reads the mask straight from SGPRs)
-    const uint32_t at = sel_mask(m, ((uint32_t)rank_below(m) << 2) + qend,
-                                 (uint32_t)(kCandOff + 4 * lane));
-    *reinterpret_cast<uint32_t *>(S.buf + at) = (uint32_t)(4 * (64 * r + lane));
-    qend += 4u * (uint32_t)__popcll(m);
-  }
-  const int qwr = (int)(qend - kQOff) >> 2;   // walkers queued (S.q()[0 .. qwr))
+  PROF_MARK(0);                       // index + walker queue
+  wave_sync();
+  const int qwr = (int)qn;               // walkers queued (S.q()[0 .. qwr))
   wave_sync();
 
   PROF_MARK(1);                       // walker queue
@@ -762,7 +791,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
 template <bool kAligned>   // the input is 4-byte aligned (the host checks)
 __global__ __launch_bounds__(64) void lz4_tiles(
     const uint8_t *__restrict__ in, uint32_t nb, uint32_t per, uint32_t last_n,
-    uint8_t *__restrict__ slots, uint32_t *__restrict__ usz, uint16_t *__restrict__ bsizes) {
+    uint8_t *__restrict__ slots, uint32_t *__restrict__ usz, uint16_t *__restrict__ bsizes,
+    uint32_t *__restrict__ status) {
   __shared__ TileLds S;
   const int lane = threadIdx.x;
   // XCD-aware order: workgroups w and w + 8 share an XCD (observed round-robin
@@ -795,8 +825,8 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   wave_sync();
 
   uint32_t *const recs = reinterpret_cast<uint32_t *>(slots + (size_t)t * kSlot);
-  const int W = n == kBlk ? encode_block<false, true>(S, n, nullptr, recs)
-                          : encode_block<false, false>(S, n, nullptr, recs);
+  const int W = n == kBlk ? encode_block<false, true>(S, n, nullptr, recs, status)
+                          : encode_block<false, false>(S, n, nullptr, recs, status);
   if (lane == 0) {
     usz[t] = (uint32_t)W;
     bsizes[t] = (uint16_t)W;
@@ -816,7 +846,7 @@ __global__ __launch_bounds__(64) void lz4_matches(const uint8_t *__restrict__ in
   for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
   if (lane < 16) S.buf[kInOff + n + lane] = 0;
   wave_sync();
-  encode_block<true, false>(S, n, mout + (size_t)t * kBlk, nullptr);
+  encode_block<true, false>(S, n, mout + (size_t)t * kBlk, nullptr, nullptr);
 }
 
 // find_longest_match over a block of any length n (block_encode with a
@@ -1190,7 +1220,8 @@ struct lz4r_ctx {
   uint32_t *tsz = nullptr;     // encoded bytes per block (u32, for the scan)
   uint32_t *gsum = nullptr;    // encoded bytes per group of kGT blocks
   uint64_t *part = nullptr;    // scan partials, one per kPart blocks
-  uint64_t *len = nullptr;     // default device length slot
+  uint64_t *len = nullptr;     // default device length slot, then the status word
+  uint32_t *status = nullptr;  // (len + 1) nonzero once a block saw a corrupt bucket head
   size_t last_nb = 0;
   // timing: the call's start/end, and lz4_tiles' start/end in every chunk
   hipEvent_t ev_a = nullptr, ev_c = nullptr;
@@ -1284,10 +1315,12 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
     // (every chunk starts 300 b0 bytes in: a multiple of 4)
     if (((uintptr_t)in & 3) == 0)
       hipLaunchKernelGGL(lz4_tiles<true>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
-                         (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0);
+                         (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0,
+                         c->status);
     else
       hipLaunchKernelGGL(lz4_tiles<false>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
-                         (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0);
+                         (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0,
+                         c->status);
     if (timed) (void)hipEventRecord(c->ev_tiles[2 * k + 1], s);
     const size_t p0 = b0 / kPart, np = (nbc + kPart - 1) / kPart;
     hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)np), dim3(256), 0, s, c->tsz, b1, p0,
@@ -1331,11 +1364,13 @@ int lz4r_ctx_create(lz4r_ctx **out) {
   lz4r_ctx *c = new (std::nothrow) lz4r_ctx();
   if (!c) return LZ4R_ERR_NOMEM;
   if (hipGetDevice(&c->device) != hipSuccess ||
-      hipMalloc(&c->len, sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&c->len, 2 * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->len, 0, 2 * sizeof(uint64_t)) != hipSuccess ||
       hipEventCreate(&c->ev_a) != hipSuccess || hipEventCreate(&c->ev_c) != hipSuccess) {
     lz4r_ctx_destroy(c);
     return LZ4R_ERR_HIP;
   }
+  c->status = reinterpret_cast<uint32_t *>(c->len + 1);
   *out = c;
   return LZ4R_OK;
 }
@@ -1381,16 +1416,20 @@ int lz4r_compress_device(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, s
   if (!c || !out_len) return LZ4R_ERR_ARG;
   int rc = run(c, d_in, n, d_out, cap, c->len, 1, stream);
   if (rc != LZ4R_OK) return rc;
-  uint64_t need = 0;
+  uint64_t got[2] = {0, 0};            // the length and the status word: one read-back
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipError_t e = hipMemcpyAsync(&need, c->len, sizeof(need), hipMemcpyDeviceToHost, s);
+  hipError_t e = hipMemcpyAsync(got, c->len, sizeof(got), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     if (getenv("LZ4R_DEBUG")) fprintf(stderr, "lz4r: %s\n", hipGetErrorString(e));
     return LZ4R_ERR_HIP;
   }
-  *out_len = (size_t)need;
-  return need > cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
+  *out_len = (size_t)got[0];
+  if ((uint32_t)got[1] != 0) {           // a corrupt bucket head: clear it, report it
+    (void)hipMemset(c->status, 0, sizeof(uint32_t));
+    return LZ4R_ERR_CORRUPT;
+  }
+  return got[0] > cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
 }
 
 int lz4r_block_matches_device(const void *d_in, size_t n, void *d_matches, void *stream) {
@@ -1476,6 +1515,18 @@ int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t 
   (void)hipFree(dout);
   lz4r_ctx_destroy(c);
   return rc;
+}
+
+int lz4r_check(lz4r_ctx *c, void *stream) {
+  if (!c) return LZ4R_ERR_ARG;
+  uint32_t st = 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipMemcpyAsync(&st, c->status, sizeof(st), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return LZ4R_ERR_HIP;
+  if (st == 0) return LZ4R_OK;
+  (void)hipMemset(c->status, 0, sizeof(uint32_t));
+  return LZ4R_ERR_CORRUPT;
 }
 
 int lz4r_set_timing(lz4r_ctx *c, int enable) {

@@ -123,6 +123,13 @@ class Compressor:
             _raise(rc, "lz4r_block_offsets_device")
         return ptr.value, cnt.value
 
+    def check(self, stream=None):
+        """lz4r_check: synchronise and raise Lz4Error(-6) if a call since the
+        last check met a corrupt bucket head (compress_device checks itself)."""
+        rc = _lib.lib().lz4r_check(self._h, _stream_handle(stream))
+        if rc != 0:
+            _raise(rc, "lz4r_check")
+
     def set_timing(self, enable=True):
         """Record HIP events on the launch stream around each call and its
         match-finder/parse kernel (see last_timing)."""

@@ -11,7 +11,8 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $O/bench.json 2> $O/be
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.log && \
 python3 tools/prof_summary.py $O/prof > $O/kernels.md && \
 bash tools/traffic.sh > $O/traffic.log 2>&1 && cp gpurun_out/traffic/traffic.json $O/traffic.json && \
-bash tools/issue.sh > $O/issue.log 2>&1 && cp gpurun_out/issue/issue.json $O/issue.json
+bash tools/issue.sh > $O/issue.log 2>&1 && cp gpurun_out/issue/issue.json $O/issue.json && \
+bash tools/clock_pmc.sh > $O/clock.json 2> $O/clock.log
 rc=$?
 tail -2 $O/tests.log; grep -E "^\[bench\]" $O/bench.err | tail -12; cat $O/kernels.md
 exit $rc

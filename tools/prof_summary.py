@@ -13,10 +13,20 @@ import sys
 
 
 def from_db(path):
+    """Per kernel and launch grid (a kernel launched over different grid sizes
+    -- e.g. lz4_tiles over the 1 GiB bench corpus and over the 8 GiB config-4
+    share -- gets one row per grid, labelled with it)."""
     c = sqlite3.connect(path)
-    rows = c.execute("select name, count(*), avg(end-start), min(end-start), max(end-start), "
-                     "sum(end-start) from kernels group by name order by sum(end-start) desc")
-    return [(r[0], r[1], r[2], r[3], r[4], r[5]) for r in rows]
+    grids = dict(c.execute("select name, count(distinct grid_x * 65536 + grid_y) from kernels "
+                           "group by name"))
+    rows = c.execute("select name, grid_x, grid_y, count(*), avg(end-start), min(end-start), "
+                     "max(end-start), sum(end-start) from kernels group by name, grid_x, grid_y "
+                     "order by sum(end-start) desc")
+    out = []
+    for name, gx, gy, n, avg, mn, mx, tot in rows:
+        label = name + (f" [grid {gx}x{gy}]" if grids[name] > 1 else "")
+        out.append((label, n, avg, mn, mx, tot))
+    return out
 
 
 def from_csv(path):
@@ -38,8 +48,9 @@ def main(path):
     print("| kernel | launches | avg us | min us | max us | total ms |")
     print("|---|---|---|---|---|---|")
     for name, n, avg, mn, mx, tot in rows:
+        grid = name[name.index(" [grid"):] if " [grid" in name else ""
         short = name.replace("(anonymous namespace)::", "").split("(")[0]
-        short = short.replace("void ", "")
+        short = short.replace("void ", "") + grid
         print(f"| `{short}` | {n} | {avg / 1e3:.1f} | {mn / 1e3:.1f} | {mx / 1e3:.1f} | "
               f"{tot / 1e6:.3f} |")
 
