@@ -17,20 +17,22 @@
 // full binary tree listed left to right, so the codes follow from the lengths
 // (code[k] = (code[k-1] + 1) shifted to len[k]; left-aligned they increase).
 //
-// Mapping: one LANE per stream (a stream's work is a few hundred serial
-// steps; a wave per stream would issue each serial step for 64 lanes).  A
-// workgroup is one wave holding 64 tiles' streams of ONE channel, so Y
-// (64 ints, ~100 RLE symbols) and chroma (32 ints) never share a wave.  The
-// per-lane working set (symbol hash, heap with counts, tree, codes) lives
-// in LDS laid out dword-column-per-lane, sized for <= 24 distinct symbols
-// (luma) / 12 (chroma) (random 4K tiles: Y <= 21, chroma <= 10): 19.5 / 10 KB
-// per wave, 8 / 16 waves per CU; a stream with more is deferred to a second
-// pass with the same code over global-memory scratch and room for 128.
-// The encoder is bound by the instructions of its longest lane (every loop
-// runs to the wave's maximum trip count) and the memory round trips of its
-// stream reads: 32 streams per wave instead of 64 measured slower (0.29 ->
-// 0.32 ms), reading each stream as 16-B chunks ahead of the RLE walk faster
-// (0.29 -> 0.25 ms per 4K image; 0.42 before the smaller working set).
+// Mapping: one LANE per stream (a stream's Huffman build is a few hundred
+// dependent steps; a wave per stream would issue each serial step for 64
+// lanes).  A workgroup is one wave holding 64 tiles' streams of ONE channel,
+// so Y (64 ints, ~100 RLE symbols) and chroma (32 ints) never share a wave.
+// The per-lane working set lives in LDS laid out dword-column-per-lane (every
+// lane owns its bank whatever index it uses).  The fast encoder
+// (entropy_encode_lane) maps symbols through a direct per-lane table, so its
+// RLE + count walk does one LDS round trip per position instead of a probe
+// chain per symbol, and keeps each emission's leaf ids in registers for the
+// sequence pass: 0.25 -> 0.14 ms per 4K image.  (A wave-cooperative RLE and
+// sequence -- one stream per wave step, ballots and LDS atomics -- measured
+// 0.34 ms: 64 dependent steps per wave, same-address atomics serialised.)
+// Streams with a symbol outside the table or more than 24 (luma) / 12
+// (chroma) distinct symbols (random 4K tiles: Y <= 21, chroma <= 10) go to a
+// second pass running the hashed encoder over global-memory scratch with
+// room for 128.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -132,6 +134,56 @@ __device__ __forceinline__ void heapify(const W &w, int size, int i) {
   w.heap[i + 1] = x;
 }
 
+// The Huffman code of one stream from its U symbols' counts, exactly as the
+// reference builds it: build_heap (JPEG.c:913-936) over the frequency list in
+// first-occurrence order, build_huffman_tree (:938-962: pop, pop, append the
+// merged node WITHOUT sifting it up), assign_codes (:964-983: DFS, left
+// first).  In: w.heap[u + 1] = count << 8 | u and w.sym[u] for u < U.  Out:
+// w.code / w.len per leaf and the table (value | length << 16 per code, DFS
+// order).  Returns true when a code exceeds the reference's char code[32].
+template <class W>
+__device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
+  for (int i = U / 2 - 1; i >= 0; --i) heapify(w, U, i);
+  int size = U, next = U;
+  while (size > 1) {
+    const uint16_t left = w.heap[1];
+    w.heap[1] = w.heap[size--];
+    heapify(w, size, 0);
+    const uint16_t right = w.heap[1];
+    w.heap[1] = w.heap[size--];
+    heapify(w, size, 0);
+    w.heap[size + 1] = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next);   // not sifted up
+    w.heap[U - (next - U)] = (uint16_t)((left & 255) | ((right & 255) << 8));   // freed slot
+    ++size;
+    ++next;
+  }
+
+  // ---- codes: DFS, left first (JPEG.c:964-983) ------------------------------
+  // Leaves pop in codes[] order; each code follows from the previous one:
+  // code[k] = (code[k-1] + 1) moved to length len[k].
+  bool over = false;
+  int sp = 0, k = 0, plen = 0;
+  uint32_t pcode = 0;
+  w.stk[sp++] = (uint16_t)(w.heap[1] & 255);         // root, depth 0
+  while (sp) {
+    const int e = w.stk[--sp];
+    const int x = e & 255, d = e >> 8;
+    if (x < U) {                                      // leaf: next entry of codes[]
+      if (k) pcode = d >= plen ? (pcode + 1) << (d - plen) : (pcode + 1) >> (plen - d);
+      plen = d;
+      w.code[x] = pcode;
+      w.len[x] = (uint8_t)d;
+      if (d > 31) over = true;                        // char code[32] (JPEG.c:861)
+      table[k++] = (uint16_t)w.sym[x] | ((uint32_t)d << 16);
+      continue;
+    }
+    const int ch = w.heap[2 * U - x];               // children of merged node x - U
+    w.stk[sp++] = (uint16_t)((ch >> 8) | ((d + 1) << 8));      // right, visited second
+    w.stk[sp++] = (uint16_t)((ch & 255) | ((d + 1) << 8));     // left first
+  }
+  return over;
+}
+
 enum : int { kOk = 0, kDefer = 1, kOverflow = 2 };
 
 __device__ __forceinline__ int hash_slot(int s, int mask) {
@@ -220,45 +272,8 @@ __device__ int encode_stream(const int16_t *__restrict__ zz, int n, const W &w,
   });
   if (defer) return kDefer;
 
-  // ---- heap and tree (JPEG.c:913-962) -------------------------------------
-  for (int i = U / 2 - 1; i >= 0; --i) heapify(w, U, i);
-  int size = U, next = U;
-  while (size > 1) {
-    const uint16_t left = w.heap[1];
-    w.heap[1] = w.heap[size--];
-    heapify(w, size, 0);
-    const uint16_t right = w.heap[1];
-    w.heap[1] = w.heap[size--];
-    heapify(w, size, 0);
-    w.heap[size + 1] = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next);   // not sifted up
-    w.heap[U - (next - U)] = (uint16_t)((left & 255) | ((right & 255) << 8));   // freed slot
-    ++size;
-    ++next;
-  }
-
-  // ---- codes: DFS, left first (JPEG.c:964-983) ------------------------------
-  // Leaves pop in codes[] order; each code follows from the previous one:
-  // code[k] = (code[k-1] + 1) moved to length len[k].
-  bool over = false;
-  int sp = 0, k = 0, plen = 0;
-  uint32_t pcode = 0;
-  w.stk[sp++] = (uint16_t)(w.heap[1] & 255);         // root, depth 0
-  while (sp) {
-    const int e = w.stk[--sp];
-    const int x = e & 255, d = e >> 8;
-    if (x < U) {                                      // leaf: next entry of codes[]
-      if (k) pcode = d >= plen ? (pcode + 1) << (d - plen) : (pcode + 1) >> (plen - d);
-      plen = d;
-      w.code[x] = pcode;
-      w.len[x] = (uint8_t)d;
-      if (d > 31) over = true;                        // char code[32] (JPEG.c:861)
-      table[k++] = (uint16_t)w.sym[x] | ((uint32_t)d << 16);
-      continue;
-    }
-    const int ch = w.heap[2 * U - x];               // children of merged node x - U
-    w.stk[sp++] = (uint16_t)((ch >> 8) | ((d + 1) << 8));      // right, visited second
-    w.stk[sp++] = (uint16_t)((ch & 255) | ((d + 1) << 8));     // left first
-  }
+  // ---- heap, tree and codes (JPEG.c:913-983) ---------------------------------
+  bool over = tree_codes(w, U, table);
 
   // ---- encoded sequence, MSB-first (JPEG.c:993-1007): RLE again --------------
   uint64_t acc = 0;
@@ -290,51 +305,180 @@ __device__ int encode_stream(const int16_t *__restrict__ zz, int n, const W &w,
 template <typename T>
 using GColT = Col<T>;
 
-// dword-column blocks ([rows][64] u32), rows = elements * size / 4
-template <int Cap, int Hash>
-struct FastLds {
-  uint32_t sym[Cap / 2][kLanes];
-  uint32_t hash[Hash / 4][kLanes];
-  uint32_t heap[(Cap + 2) / 2][kLanes];
-  uint32_t code[Cap][kLanes];
-  uint32_t len[Cap / 4][kLanes];
-  uint32_t stk[(Cap + 2) / 2][kLanes];
-};
-
 // scratch header (in d_scratch): [0] deferred count, then the deferred list
 struct ScratchHdr {
   uint32_t ndefer;
   uint32_t pad[3];
 };
 
-// Luma streams (64 ints, up to ~21 distinct symbols on noise) get room for
-// kFastCap symbols; chroma streams (32 ints, <= ~10) for kChromaCap, half the
-// LDS and so twice the waves per CU.  Streams with more symbols are deferred.
+// ---- the fast encoder: one lane per stream, no probing ------------------------
+// Symbols index a direct per-lane table (symbol + kOff -> leaf + 1, u8), so a
+// lookup is one LDS read with no probe loop: the RLE walk is unrolled over
+// the stream's positions and, per position, every lane whose run ends there
+// looks up BOTH its symbols (count, value) with the two reads in flight
+// together (an equal pair is resolved in registers) -- one LDS round trip
+// per position, where the hashed walk took up to three per symbol, for the
+// wave's longest probe chain.  Counts are bumped by ds_add_u32 on the heap
+// entry's half-word (no read).  Each emission's two leaf ids stay in
+// registers (5 bits each, 3 positions per dword), so the sequence pass reads
+// only the codes.  The table is dead after the count: the DFS stack and the
+// codes overlay it.  A stream with a symbol outside the table or more than
+// Cap distinct symbols is deferred to entropy_encode_deferred.
+template <int N>
+struct LaneLds {
+  static constexpr int Cap = N == 64 ? kFastCap : kChromaCap;
+  static constexpr int Keys = N == 64 ? 176 : 120;   // symbols [-Off, Keys - Off)
+  static constexpr int Off = N == 64 ? 64 : 48;       // counts: 1 .. N
+  static constexpr int StkRows = (Cap + 2) / 2;       // overlays of the table (dword rows)
+  static constexpr int CodeRow = StkRows, LenRow = StkRows + Cap;
+  static_assert(LenRow + Cap / 4 <= Keys / 4, "stack, codes and lengths fit the table");
+  static_assert(Off + N < Keys, "every count is a key");
+  uint32_t tab[Keys / 4][kLanes];
+  uint32_t heap[(Cap + 2) / 2][kLanes];
+  uint32_t sym[Cap / 4][kLanes];                      // int8 symbols
+};
+
+struct LaneWork {                                     // the arrays tree_codes uses
+  LCol<int8_t> sym;
+  LCol<uint16_t> heap;
+  LCol<uint32_t> code;
+  LCol<uint8_t> len;
+  LCol<uint16_t> stk;
+};
+
 template <bool kLuma>
-__global__ __launch_bounds__(kLanes) void entropy_encode_fast(
+__global__ __launch_bounds__(kLanes) void entropy_encode_lane(
     const int16_t *__restrict__ coef, size_t ntiles, uint8_t *__restrict__ bits,
     uint32_t *__restrict__ meta, uint32_t *__restrict__ table, ScratchHdr *__restrict__ hdr,
     uint32_t *__restrict__ deferred, uint32_t *__restrict__ status) {
-  constexpr int Cap = kLuma ? kFastCap : kChromaCap;
-  constexpr int Hash = kLuma ? 32 : 16;
-  __shared__ FastLds<Cap, Hash> S;
+  constexpr int N = kLuma ? 64 : 32;
+  using L = LaneLds<N>;
+  constexpr int Cap = L::Cap, Keys = L::Keys, Off = L::Off;
+  __shared__ L S;
   const int lane = threadIdx.x;
   const int c = kLuma ? 0 : 1 + (int)(blockIdx.x & 1);      // channel of this wave
   const size_t tile = (size_t)(kLuma ? blockIdx.x : blockIdx.x >> 1) * kLanes + lane;
   if (tile >= ntiles) return;
-  auto col = [&](uint32_t(*blk)[kLanes]) { return reinterpret_cast<uint8_t *>(&blk[0][lane]); };
-  const Work<LCol> w{{col(S.sym)}, {col(S.hash)}, {col(S.heap)},
-                     {col(S.code)}, {col(S.len)}, {col(S.stk)}};
-  const int rc = encode_stream<Cap, Hash>(
-      coef + tile * 128 + coef_off(c), stream_len(c), w, bits + tile * kBitsPerTile + bits_off(c),
-      bits_cap(c), ref_bits_max(c), table + tile * kTablePerTile + bits_off(c),
-      meta + tile * 3 + c);
-  if (rc == kDefer) {
+  auto colp = [&](uint32_t *row0) { return reinterpret_cast<uint8_t *>(row0 + lane); };
+  uint8_t *const tabc = colp(&S.tab[0][0]);
+  const LaneWork w{{colp(&S.sym[0][0])}, {colp(&S.heap[0][0])},
+                   {colp(&S.tab[L::CodeRow][0])}, {colp(&S.tab[L::LenRow][0])},
+                   {colp(&S.tab[0][0])}};
+
+  // the stream: N int16 as N / 2 packed dwords (16-B loads)
+  uint32_t iw[N / 2];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(coef + tile * 128 + coef_off(c));
+#pragma unroll
+    for (int k = 0; k < N / 8; ++k) {
+      const uint4 q = src[k];
+      iw[4 * k] = q.x; iw[4 * k + 1] = q.y; iw[4 * k + 2] = q.z; iw[4 * k + 3] = q.w;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < Keys / 4; ++r) *reinterpret_cast<uint32_t *>(tabc + r * (4 * kLanes)) = 0u;
+  auto val = [&](int i) { return (int)(int16_t)(iw[i >> 1] >> (16 * (i & 1))); };
+  auto tab_at = [&](int k) -> uint8_t & {
+    return *(tabc + (k >> 2) * (4 * kLanes) + (k & 3));
+  };
+  auto heap_dw = [&](int slot) {
+    return reinterpret_cast<uint32_t *>(w.heap.p + (slot >> 1) * (4 * kLanes));
+  };
+
+  // ---- RLE (JPEG.c:767-808) + frequencies (JPEG.c:864-886) ------------------
+  // run k ends at position i when i == N - 1 or the next int differs; it
+  // emits (count, value).  Leaf ids in first-occurrence order.
+  uint32_t lid[(N + 2) / 3];             // per position: (leaf_c + 1) | (leaf_v + 1) << 5
+#pragma unroll
+  for (int j = 0; j < (N + 2) / 3; ++j) lid[j] = 0;
+  int U = 0, start = 0;
+  bool defer = false;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int v = val(i);
+    const bool end = i == N - 1 || val(i + 1 < N ? i + 1 : i) != v;
+    if (end && !defer) {
+      const int kc = i + 1 - start + Off, kv = v + Off;
+      start = i + 1;
+      if ((uint32_t)kv >= (uint32_t)Keys) {
+        defer = true;
+      } else {
+        const int ec = tab_at(kc), ev = tab_at(kv);     // both reads in flight
+        const bool same = kv == kc;
+        const int lc = ec ? ec - 1 : U;
+        const int nu = U + (ec ? 0 : 1);
+        const int lv = same ? lc : (ev ? ev - 1 : nu);
+        const int nu2 = nu + ((same || ev) ? 0 : 1);
+        if (nu2 > Cap) {
+          defer = true;
+        } else {
+          // new leaves: table entry, symbol, heap entry (count << 8 | id);
+          // known ones: +1 on the count (ds_add on the entry's half-word)
+          if (!ec) {
+            tab_at(kc) = (uint8_t)(lc + 1);
+            w.sym[lc] = (int8_t)(kc - Off);
+            w.heap[lc + 1] = (uint16_t)(((same ? 2 : 1) << 8) | lc);
+          } else {
+            atomicAdd(heap_dw(lc + 1), (same ? 512u : 256u) << (16 * ((lc + 1) & 1)));
+          }
+          if (!same) {
+            if (!ev) {
+              tab_at(kv) = (uint8_t)(lv + 1);
+              w.sym[lv] = (int8_t)v;
+              w.heap[lv + 1] = (uint16_t)((1 << 8) | lv);
+            } else {
+              atomicAdd(heap_dw(lv + 1), 256u << (16 * ((lv + 1) & 1)));
+            }
+          }
+          U = nu2;
+          lid[i / 3] |= (uint32_t)((lc + 1) | ((lv + 1) << 5)) << (10 * (i % 3));
+        }
+      }
+    }
+  }
+  if (defer) {
     const uint32_t slot = atomicAdd(&hdr->ndefer, 1u);
     deferred[slot] = (uint32_t)(tile * 3 + c);
-  } else if (rc == kOverflow) {
-    atomicAdd(&status[0], 1u);
+    return;
   }
+  int R = 0;
+#pragma unroll
+  for (int j = 0; j < (N + 2) / 3; ++j)
+    R += (lid[j] & 1023u ? 2 : 0) + ((lid[j] >> 10) & 1023u ? 2 : 0) + ((lid[j] >> 20) & 1023u ? 2 : 0);
+
+  // ---- heap, tree and codes (JPEG.c:913-983): the table is dead ------------
+  bool over = tree_codes(w, U, table + tile * kTablePerTile + bits_off(c));
+
+  // ---- encoded sequence, MSB-first (JPEG.c:993-1007) ------------------------
+  uint32_t *const wout = reinterpret_cast<uint32_t *>(bits + tile * kBitsPerTile + bits_off(c));
+  constexpr int nwords = N / 2;                       // bits_cap / 32
+  uint64_t acc = 0;
+  int nacc = 0, nbits = 0, word = 0;
+  auto put = [&](int id) {                            // id = leaf + 1, 0: nothing
+    const int leaf = id ? id - 1 : 0;
+    const uint32_t cd = w.code[leaf];
+    const int Lb = id ? (int)w.len[leaf] : 0;
+    acc = (acc << Lb) | (id ? cd : 0u);
+    nacc += Lb;
+    nbits += Lb;
+    if (nacc >= 32) {
+      const uint32_t v = (uint32_t)(acc >> (nacc - 32));
+      if (word < nwords) wout[word] = __builtin_bswap32(v);
+      ++word;
+      nacc -= 32;
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t id = (lid[i / 3] >> (10 * (i % 3))) & 1023u;
+    put((int)(id & 31u));
+    put((int)(id >> 5));
+  }
+  if (nacc && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc << (32 - nacc)));
+  if (nbits > ref_bits_max(c)) over = true;           // char sequence[1024] / [512]
+  meta[tile * 3 + c] = (uint32_t)(nbits < 0xFFFF ? nbits : 0xFFFF) | ((uint32_t)R << 16) |
+                       ((uint32_t)U << 24);
+  if (over) atomicAdd(&status[0], 1u);
 }
 
 __global__ __launch_bounds__(kLanes) void entropy_encode_deferred(
@@ -570,11 +714,11 @@ extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, vo
   auto *status = static_cast<uint32_t *>(d_status);
   hipLaunchKernelGGL(entropy_init, dim3(1), dim3(1), 0, s, hdr, status);
   const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
-  hipLaunchKernelGGL(entropy_encode_fast<true>, dim3(groups), dim3(kLanes), 0, s,
+  hipLaunchKernelGGL(entropy_encode_lane<true>, dim3(groups), dim3(kLanes), 0, s,
                      static_cast<const int16_t *>(d_coef), ntiles, static_cast<uint8_t *>(d_bits),
                      static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
                      deferred, status);
-  hipLaunchKernelGGL(entropy_encode_fast<false>, dim3(groups * 2), dim3(kLanes), 0, s,
+  hipLaunchKernelGGL(entropy_encode_lane<false>, dim3(groups * 2), dim3(kLanes), 0, s,
                      static_cast<const int16_t *>(d_coef), ntiles, static_cast<uint8_t *>(d_bits),
                      static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
                      deferred, status);

@@ -9,7 +9,7 @@ C2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT
 timeout -k 10 120 rocprofv3 --kernel-trace --pmc $C1 -d $O/a -o run -- python3 tools/ent_one.py 3 > $O/a.log 2>&1 && \
 timeout -k 10 120 rocprofv3 --kernel-trace --pmc $C2 -d $O/b -o run -- python3 tools/ent_one.py 3 > $O/b.log 2>&1
 rc=$?
-for k in "entropy_encode_fast<true>" "entropy_encode_fast<false>" "entropy_decode_kernel<true>"; do
+for k in "entropy_encode_lane<true>" "entropy_encode_lane<false>" "entropy_decode_kernel<true>"; do
   echo "== $k"
   python3 tools/pmc_summary.py $O/a/run_results.db "$k" | tail -9
   python3 tools/pmc_summary.py $O/b/run_results.db "$k" | tail -7
