@@ -109,29 +109,48 @@ struct Work {
   A<uint16_t> stk;      // [Cap + 1]   DFS stack: node | depth << 8
 };
 
-// Sift the entry at i down (JPEG.c:895-911: smallest of i, left, right by
-// count with strict <, left tested first), holding it in registers and
-// moving children up into the hole -- the same final arrangement as the
-// reference's swaps.
-template <class W>
-__device__ __forceinline__ void heapify(const W &w, int size, int i) {
-  const uint16_t x = w.heap[i + 1];
+// Sift x down from index i (JPEG.c:895-911: smallest of i, left, right by
+// count with strict <, left tested first), moving children up into the hole
+// -- the same final arrangement as the reference's swaps.  x is passed in
+// registers (slot i is not read), and each LDS round trip serves two levels:
+// the children pair and both grandchildren pairs are read together.  Slots
+// past MaxSlot (the array's last even slot) are clamped: such a pair is never
+// used.  Returns the entry left at index i (for the root: the new minimum).
+template <int MaxSlot, class W>
+__device__ __forceinline__ uint16_t sift(const W &w, int size, int i, uint16_t x) {
   const int cx = x >> 8;
+  uint16_t top = x;
+  bool moved = false;
   for (;;) {
     const int l = 2 * i + 1, r = l + 1;
     if (l >= size) break;
-    const uint32_t pr = w.heap.pair(l + 1);           // entries l, r: slots l + 1 (even), l + 2
-    const uint16_t hl = (uint16_t)pr;
-    const uint16_t hr = r < size ? (uint16_t)(pr >> 16) : (uint16_t)0xFFFF;
+    const uint32_t pc = w.heap.pair(l + 1);               // entries l, r (slots l + 1, l + 2)
+    const uint32_t pgl = w.heap.pair(min(2 * l + 2, MaxSlot));   // l's children
+    const uint32_t pgr = w.heap.pair(min(2 * l + 4, MaxSlot));   // r's children
+    const uint16_t hl = (uint16_t)pc, hr = (uint16_t)(pc >> 16);
     int s = i, cs = cx;
     uint16_t hs = x;
     if ((hl >> 8) < cs) { s = l; cs = hl >> 8; hs = hl; }
     if (r < size && (hr >> 8) < cs) { s = r; hs = hr; }
     if (s == i) break;
     w.heap[i + 1] = hs;
+    if (!moved) top = hs;
+    moved = true;
     i = s;
+    const int l2 = 2 * i + 1;                             // the next level, prefetched
+    if (l2 >= size) break;
+    const uint32_t pg = s == l ? pgl : pgr;
+    const uint16_t gl = (uint16_t)pg, gr = (uint16_t)(pg >> 16);
+    int s2 = i, c2 = cx;
+    uint16_t h2 = x;
+    if ((gl >> 8) < c2) { s2 = l2; c2 = gl >> 8; h2 = gl; }
+    if (l2 + 1 < size && (gr >> 8) < c2) { s2 = l2 + 1; h2 = gr; }
+    if (s2 == i) break;
+    w.heap[i + 1] = h2;
+    i = s2;
   }
   w.heap[i + 1] = x;
+  return top;
 }
 
 // The Huffman code of one stream from its U symbols' counts, exactly as the
@@ -141,32 +160,38 @@ __device__ __forceinline__ void heapify(const W &w, int size, int i) {
 // first).  In: w.heap[u + 1] = count << 8 | u and w.sym[u] for u < U.  Out:
 // w.code / w.len per leaf and the table (value | length << 16 per code, DFS
 // order).  Returns true when a code exceeds the reference's char code[32].
-template <class W>
+template <int Cap, class W>
 __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
-  for (int i = U / 2 - 1; i >= 0; --i) heapify(w, U, i);
+  constexpr int kMaxSlot = Cap & ~1;                  // heap slots 0 .. Cap + 1
+  for (int i = U / 2 - 1; i >= 0; --i) sift<kMaxSlot>(w, U, i, w.heap[i + 1]);
   int size = U, next = U;
+  uint16_t root = w.heap[1];
   while (size > 1) {
-    const uint16_t left = w.heap[1];
-    w.heap[1] = w.heap[size--];
-    heapify(w, size, 0);
-    const uint16_t right = w.heap[1];
-    w.heap[1] = w.heap[size--];
-    heapify(w, size, 0);
-    w.heap[size + 1] = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next);   // not sifted up
+    // pop, pop (the moved last entry sifted from the root; the new root is
+    // known in registers), append the merged node unsifted
+    const uint16_t left = root;
+    --size;
+    root = sift<kMaxSlot>(w, size, 0, w.heap[size + 1]);
+    const uint16_t right = root;
+    --size;
+    root = sift<kMaxSlot>(w, size, 0, w.heap[size + 1]);
+    const uint16_t merged = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next);
+    w.heap[size + 1] = merged;                                              // not sifted up
     w.heap[U - (next - U)] = (uint16_t)((left & 255) | ((right & 255) << 8));   // freed slot
     ++size;
     ++next;
+    if (size == 1) root = merged;
   }
 
   // ---- codes: DFS, left first (JPEG.c:964-983) ------------------------------
   // Leaves pop in codes[] order; each code follows from the previous one:
-  // code[k] = (code[k-1] + 1) moved to length len[k].
+  // code[k] = (code[k-1] + 1) moved to length len[k].  The current node stays
+  // in registers: an internal node stacks its right child and descends left.
   bool over = false;
   int sp = 0, k = 0, plen = 0;
   uint32_t pcode = 0;
-  w.stk[sp++] = (uint16_t)(w.heap[1] & 255);         // root, depth 0
-  while (sp) {
-    const int e = w.stk[--sp];
+  int e = root & 255;                                 // the root, depth 0
+  for (;;) {
     const int x = e & 255, d = e >> 8;
     if (x < U) {                                      // leaf: next entry of codes[]
       if (k) pcode = d >= plen ? (pcode + 1) << (d - plen) : (pcode + 1) >> (plen - d);
@@ -175,11 +200,13 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
       w.len[x] = (uint8_t)d;
       if (d > 31) over = true;                        // char code[32] (JPEG.c:861)
       table[k++] = (uint16_t)w.sym[x] | ((uint32_t)d << 16);
-      continue;
+      if (sp == 0) break;
+      e = w.stk[--sp];
+    } else {
+      const int ch = w.heap[2 * U - x];               // children of merged node x - U
+      w.stk[sp++] = (uint16_t)((ch >> 8) | ((d + 1) << 8));   // right, visited later
+      e = (ch & 255) | ((d + 1) << 8);                         // left now
     }
-    const int ch = w.heap[2 * U - x];               // children of merged node x - U
-    w.stk[sp++] = (uint16_t)((ch >> 8) | ((d + 1) << 8));      // right, visited second
-    w.stk[sp++] = (uint16_t)((ch & 255) | ((d + 1) << 8));     // left first
   }
   return over;
 }
@@ -273,7 +300,7 @@ __device__ int encode_stream(const int16_t *__restrict__ zz, int n, const W &w,
   if (defer) return kDefer;
 
   // ---- heap, tree and codes (JPEG.c:913-983) ---------------------------------
-  bool over = tree_codes(w, U, table);
+  bool over = tree_codes<Cap>(w, U, table);
 
   // ---- encoded sequence, MSB-first (JPEG.c:993-1007): RLE again --------------
   uint64_t acc = 0;
@@ -447,7 +474,7 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
     R += (lid[j] & 1023u ? 2 : 0) + ((lid[j] >> 10) & 1023u ? 2 : 0) + ((lid[j] >> 20) & 1023u ? 2 : 0);
 
   // ---- heap, tree and codes (JPEG.c:913-983): the table is dead ------------
-  bool over = tree_codes(w, U, table + tile * kTablePerTile + bits_off(c));
+  bool over = tree_codes<Cap>(w, U, table + tile * kTablePerTile + bits_off(c));
 
   // ---- encoded sequence, MSB-first (JPEG.c:993-1007) ------------------------
   uint32_t *const wout = reinterpret_cast<uint32_t *>(bits + tile * kBitsPerTile + bits_off(c));

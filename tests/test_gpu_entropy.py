@@ -132,3 +132,57 @@ def test_image_vs_oracle_and_roundtrip(gpu, oracle, w, h, kind):
     torch.cuda.synchronize()
     assert int(ent.status[1].item()) == 0
     assert torch.equal(out, d_coef)
+
+
+def _boundary_streams():
+    """Luma (64-int) and chroma (32-int) streams at the fast encoder's edges:
+    the direct symbol table's key range (luma -64..111, chroma -48..71; one
+    past either end is deferred), the distinct-symbol caps (24 / 12; one more
+    is deferred), whole-stream runs (count 64 / 32), counts equal to values,
+    and symbols met first as a value and later as a count."""
+    luma = [
+        [-64, 111] * 32, [-65] + [0] * 63, [112] + [1] * 63, [5] * 64, [0] * 64,
+        [10 + (i % 23) for i in range(64)],                 # 24 distinct: count 1 + 23 values
+        [10 + (i % 24) for i in range(64)],                 # 25: deferred
+        [3, 3, 3] + [1] * 61, [2, 2, 7, 7, 7, 2] + [0] * 58,
+        [1, 2, 2, 3, 3, 3, 4, 4, 4, 4] * 6 + [-1] * 4,
+        [(i * 7) % 5 - 2 for i in range(64)],
+    ]
+    chroma = [
+        [-48, 71] * 16, [-49] + [0] * 31, [72] + [0] * 31, [9] * 32,
+        [20 + (i % 11) for i in range(32)],                 # 12 distinct
+        [20 + (i % 12) for i in range(32)],                 # 13: deferred
+        [2, 2, 1, 1, 1, 3] + [0] * 26, [(i * 3) % 4 - 1 for i in range(32)],
+    ]
+    return luma, chroma
+
+
+def test_fast_path_boundaries(gpu, oracle):
+    import torch
+    from lz4jpeg import jpeg
+    luma, chroma = _boundary_streams()
+    nt = 70                                  # a second, partial wave of tiles
+    rng = np.random.default_rng(11)
+    coef = rng.integers(-3, 4, size=(nt, 128)).astype(np.int16)
+    for t, zz in enumerate(luma):
+        coef[t, :64] = zz
+    for i, zz in enumerate(chroma):
+        coef[i, 64:96] = zz
+        coef[nt - 1 - i, 96:] = zz
+    d_coef = torch.from_numpy(coef.reshape(-1)).cuda()
+    ent = jpeg.Entropy(nt)
+    ent.encode(d_coef)
+    torch.cuda.synchronize()
+    assert int(ent.status[0].item()) == 0
+    for t in range(nt):
+        for c, sl in ((0, slice(0, 64)), (1, slice(64, 96)), (2, slice(96, 128))):
+            a = oracle_api.entropy(oracle, coef[t, sl])
+            got = ent.stream(t, c)
+            assert got["rle_len"] == len(a["rle"]), (t, c)
+            assert got["table"] == [(v, ln) for v, ln, _ in a["table"]], (t, c)
+            assert (got["nbits"], got["bits"]) == (a["nbits"], a["bits"]), (t, c)
+    out = torch.zeros_like(d_coef)
+    ent.decode(out)
+    torch.cuda.synchronize()
+    assert int(ent.status[1].item()) == 0
+    assert torch.equal(out, d_coef)

@@ -28,7 +28,7 @@ def main(d):
     for kern, run, sub in (("lz4", "lz4", "lz4_tiles"), ("lz4_emit", "lz4", "lz4_emit"),
                            ("jpeg", "jpeg", "jpeg_strip_kernel"),
                            ("lz4_decode", "dec", "lz4_decode_blocks"),
-                           ("entropy_encode", "ent", "entropy_encode_fast"),
+                           ("entropy_encode", "ent", "entropy_encode_lane"),
                            ("entropy_decode", "ent", "entropy_decode_kernel")):
         f = per_launch(os.path.join(d, f"{run}_fetch", "run_results.db"), "FETCH_SIZE", sub)
         w = per_launch(os.path.join(d, f"{run}_write", "run_results.db"), "WRITE_SIZE", sub)
