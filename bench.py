@@ -74,6 +74,23 @@ def held_clock(key):
         return None
 
 
+def settle(fn, sync, ms=60.0, chunk=8):
+    """Untimed warm-up of a sub-line until `ms` of back-to-back work has run:
+    the chip's clock ramps over ~40 ms of sustained load (a 4K single-image
+    JPEG launch takes 83.5 us over its first 100 launches and settles at
+    64.8 us after ~500, tools/jpeg_settle.py; an LZ4 call 3.19 -> 2.87 ms over
+    6 calls), so a sub-line timed after a few warm-up launches measures the
+    ramp.  Returns the number of warm-up calls.  (The top-level line keeps
+    exactly the driver's W warm-up steps.)"""
+    t0, n = time.perf_counter(), 0
+    while time.perf_counter() - t0 < ms / 1e3:
+        for _ in range(chunk):
+            fn()
+        n += chunk
+        sync()
+    return n
+
+
 def at_held_clock(achieved, peak_spec, key):
     """The spec peak rescaled to the clock `key` holds under load, and the
     fraction of that; {} when no clock profile is present."""
@@ -383,6 +400,9 @@ def run_lz4(ctx, n_total, scaling):
     _, got = lz4.decompress_device(d_out, flen, d_boff, nb_local, n + 300, d_out=d_dec)
     dec_ok = got == n and bool(torch.equal(d_dec[:n], d_in[:n]))
     torch.cuda.synchronize()
+    dec_warm = settle(lambda: lz4.decompress_device(d_out, flen, d_boff, nb_local, n + 300,
+                                                    d_out=d_dec, check=False),
+                      torch.cuda.synchronize)
     ctx.barrier()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -401,6 +421,7 @@ def run_lz4(ctx, n_total, scaling):
         "value": round(n_total / (ddt / args.steps) / 1e9, 3), "unit": "GB/s",
         "kernel": "lz4_decode_blocks", "avg_launch_ms": round(dec_kern_ms, 4),
         "roundtrip_ok": dec_ok, "offsets": "device-resident, written by lz4_emit",
+        "warmup_launches": dec_warm,
         "roofline": {
             "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
             "achieved": round((n + flen) / (dec_kern_ms / 1e3) / 1e9, 2),
@@ -415,6 +436,8 @@ def run_lz4(ctx, n_total, scaling):
     _, got = lz4.decompress_stream_device(d_out, flen, n + 300, d_out=d_dec)
     bare_ok = got == n and bool(torch.equal(d_dec[:n], d_in[:n]))
     torch.cuda.synchronize()
+    bare_warm = settle(lambda: lz4.decompress_stream_device(d_out, flen, n + 300, d_out=d_dec),
+                       torch.cuda.synchronize, chunk=2)
     ctx.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -428,6 +451,7 @@ def run_lz4(ctx, n_total, scaling):
         "metric": "LZ4 decode GB/s from the stream alone (lz4r_decompress_stream_device)",
         "value": round(n_total / (bdt / args.steps) / 1e9, 3), "unit": "GB/s",
         "call_ms": round(bdt / args.steps * 1e3, 4), "roundtrip_ok": bare_ok,
+        "warmup_calls": bare_warm,
         "note": "whole synchronous call: on-device block-boundary discovery (lz4_bare_*), "
                 "lz4_decode_blocks, one host read-back"}
     log(f"lz4 bare-stream decode: {bdt / args.steps * 1e3:.3f} ms/call, "
@@ -537,6 +561,7 @@ def run_cfg4_share(ctx, comp):
     if seg > cap:
         raise RuntimeError(f"lz4 cfg4 share: segment {seg} B exceeds {cap} B")
     torch.cuda.synchronize()
+    warm = max(1, args.warmup) + settle(step, torch.cuda.synchronize, chunk=1)
     comp.set_timing(True)
     tiles = []
     t0 = time.perf_counter()
@@ -550,7 +575,7 @@ def run_cfg4_share(ctx, comp):
     res = {
         "metric": "LZ4 compress GB/s of one GPU's share of configs[3] (8 GPUs)",
         "value": round(n / (dt / args.steps) / 1e9, 3), "unit": "GB/s",
-        "ms_per_step": round(dt / args.steps * 1e3, 4), "steps": args.steps,
+        "ms_per_step": round(dt / args.steps * 1e3, 4), "steps": args.steps, "warmup": warm,
         "bytes": n, "segment_bytes": seg, "lz4_tiles_ms": round(sum(tiles) / len(tiles), 4),
         "step": "segment compress (lz4r_compress_segment_async) + length read-back",
         "note": "the 8-GPU job's rank-0 shard [0, 8 GiB) of the 64 GiB corpus; x8 is the "
@@ -580,6 +605,8 @@ def run_jpeg(ctx, total_images, scaling):
     for _ in range(max(args.warmup, 3)):
         jpeg.encode_device(d_img, W, H, B, d_coef)
     torch.cuda.synchronize()
+    jwarm = max(args.warmup, 3) + settle(lambda: jpeg.encode_device(d_img, W, H, B, d_coef),
+                                         torch.cuda.synchronize, chunk=50 if B == 1 else 1)
     ctx.barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -603,6 +630,7 @@ def run_jpeg(ctx, total_images, scaling):
     jres = {
         "metric": "JPEG DCT+quant+zigzag Gpixel/s (bit-exact int16 coefficients)",
         "value": round(gpix, 3), "unit": "Gpixel/s", "n_gpus": world, "steps": jsteps,
+        "warmup": jwarm,
         "value_per_gpu": round(gpix / world, 3),
         "ms_per_step": round(jdt / jsteps * 1e3, 4), "higher_is_better": True,
         "scaling": scaling, "dtype": "f64",
@@ -646,6 +674,8 @@ def run_jpeg(ctx, total_images, scaling):
         jpeg.encode_device(d_bimg, W, H, NB, d_bcoef)
         b_ok = bool(torch.equal(d_bcoef[:jpeg.coef_count(W, H)], d_coef[:jpeg.coef_count(W, H)]))
         torch.cuda.synchronize()
+        bwarm = settle(lambda: jpeg.encode_device(d_bimg, W, H, NB, d_bcoef), torch.cuda.synchronize,
+                       chunk=1)
         bsteps = max(3, args.steps // 2)
         b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         b0.record(stream)
@@ -659,6 +689,7 @@ def run_jpeg(ctx, total_images, scaling):
             "metric": "JPEG DCT+quant+zigzag Gpixel/s, 128 images per launch",
             "value": round(px * NB / (bms / 1e3) / 1e9, 3), "unit": "Gpixel/s",
             "images": NB, "avg_launch_ms": round(bms, 4), "image0_equals_single": b_ok,
+            "warmup": bwarm,
             "roofline": {
                 "bound": "valu_fp64", "unit": "Tops/s", "peak": FP64_VALU_PEAK_TOPS,
                 "achieved": round(btiles * 13312 / (bms / 1e3) / 1e12, 2),
@@ -680,6 +711,8 @@ def run_jpeg(ctx, total_images, scaling):
     # reconstruction: coefficients -> reconstructed RGBA
     jpeg.reconstruct_device(d1_coef, W, H, 1, d_orig=d1_img)
     torch.cuda.synchronize()
+    rwarm = settle(lambda: jpeg.reconstruct_device(d1_coef, W, H, 1, d_orig=d1_img),
+                   torch.cuda.synchronize, chunk=50)
     r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     r0.record(stream)
     for _ in range(rsteps):
@@ -692,6 +725,7 @@ def run_jpeg(ctx, total_images, scaling):
         "metric": "JPEG reconstruction (dequant + fp64 IDCT + YCbCr->RGB) Gpixel/s",
         "value": round(px / (rec_ms / 1e3) / 1e9, 3), "unit": "Gpixel/s",
         "kernel": "jpeg_recon_kernel", "avg_launch_ms": round(rec_ms, 4), "images": 1,
+        "warmup": rwarm,
         "roofline": {
             "bound": "valu_fp64", "unit": "Tops/s", "peak": FP64_VALU_PEAK_TOPS,
             "achieved": round(t1 * 13568 / (rec_ms / 1e3) / 1e12, 2),
@@ -714,6 +748,11 @@ def run_jpeg(ctx, total_images, scaling):
     meta = ent.meta.to(torch.int64) & 0xFFFFFFFF
     sum_bits = int((meta & 0xFFFF).sum().item())
     sum_codes = int((meta >> 24).sum().item())
+
+    def ent_pair():
+        ent.encode(d1_coef)
+        ent.decode(d_back)
+    ewarm = settle(ent_pair, torch.cuda.synchronize, chunk=20)
     e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     e0.record(stream)
     for _ in range(rsteps):
@@ -729,7 +768,7 @@ def run_jpeg(ctx, total_images, scaling):
     jres["entropy"] = {
         "metric": "JPEG entropy stage (RLE + per-block Huffman, JPEG.c:767-1097) Gpixel/s",
         "value": round(px / (enc_ms / 1e3) / 1e9, 3), "unit": "Gpixel/s", "images": 1,
-        "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+        "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4), "warmup": ewarm,
         "decode_gpix_s": round(px / (dec_ms / 1e3) / 1e9, 3),
         "kernels": ["entropy_encode_lane", "entropy_encode_deferred", "entropy_decode_kernel"],
         "bits_per_pixel": round(sum_bits / px, 4), "roundtrip_ok": ent_ok,
