@@ -337,11 +337,14 @@ def run_lz4(ctx, n_total, scaling):
     n = hi - lo
     final_shard = hi == n_total
     log(f"rank {rank}: synthesising LZ4 shard [{lo}, {hi}) of {n_total} B in HBM")
+    if rank == 0 and world == 1:
+        # bounded host copy for the CPU baseline (the same bytes); made before
+        # the device input so that seconds of host work do not sit between the
+        # device synthesis and the warm-up steps (the clock ramps back up over
+        # ~40 ms of load, see settle())
+        ctx.host_text = synth.random_passages(min(n, 1 << 30), length=30000, seed=1, first=lo)
     d_in = torch.empty(n + 16, dtype=torch.uint8, device=dev)
     synth.random_passages_device(d_in, n, length=30000, seed=1, first=lo)
-    if rank == 0 and world == 1:
-        # bounded host copy for the CPU baseline (the same bytes)
-        ctx.host_text = synth.random_passages(min(n, 1 << 30), length=30000, seed=1, first=lo)
     comp = lz4.Compressor()
     # text grows by ~3.5 %; the call reports the need if a shard ever exceeds this
     cap = n + n // 8 + (1 << 20)
