@@ -21,7 +21,7 @@ HDRS    := include/lz4r.h include/jpegr.h include/lz4jpeg_compat.h include/lz4jp
            $(CSRC)/jpeg_tables.h
 OBJS    := $(B)/lz4r.o $(B)/lz4r_gpudec.o $(B)/jpegr.o $(B)/jpegr_blocks.o $(B)/jpegr_entropy.o \
            $(B)/synth.o $(B)/synth_dev.o \
-           $(B)/lz4r_decode.o $(B)/compat.o
+           $(B)/lz4r_decode.o $(B)/compat.o $(B)/compat_lz4.o
 
 all: lib bin oracle tools
 
@@ -73,11 +73,13 @@ oracle:
 
 # ASan + UBSan build of the host C (no HIP) and the oracle restatements,
 # driven by tests/sanitize/sanitize_main.c; tests/test_sanitize.py
-SAN_SRC := tests/sanitize/sanitize_main.c $(HOST)/lz4r_decode.c $(HOST)/png_io.c \
-           $(HOST)/synth.c oracle/lz4_oracle.c oracle/jpeg_oracle.c oracle/jpeg_entropy_oracle.c
+SAN_SRC := tests/sanitize/sanitize_main.c tests/sanitize/cpu_matches.c $(HOST)/lz4r_decode.c \
+           $(HOST)/png_io.c $(HOST)/synth.c $(HOST)/compat_lz4.c \
+           oracle/lz4_oracle.c oracle/jpeg_oracle.c oracle/jpeg_entropy_oracle.c
 sanitize: build/sanitize_main
 
-build/sanitize_main: $(SAN_SRC) include/lz4r.h include/lz4jpeg_synth.h
+build/sanitize_main: $(SAN_SRC) include/lz4r.h include/lz4jpeg_synth.h include/lz4jpeg_compat.h \
+                     $(HOST)/lzj_host.h
 	@mkdir -p build
 	$(CC) -O1 -g -std=gnu11 -ffp-contract=off -fno-omit-frame-pointer \
 	  -fsanitize=address,undefined -fno-sanitize-recover=all \

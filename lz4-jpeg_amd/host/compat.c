@@ -14,6 +14,7 @@
 #include "../../include/jpegr.h"
 #include "../../include/lz4jpeg_compat.h"
 #include "../../include/lz4r.h"
+#include "lzj_host.h"
 
 /* safe_open, LZ4.c:109-120 */
 static FILE *safe_open(const char *name, const char *mode) {
@@ -94,187 +95,36 @@ void lz4_encode(void) {
   dump_to_hex_file(LZ4_COMPRESSED_FILE, LZ4_HEX_FILE);
 }
 
-/* ---- per-block API: find_longest_match / block_encode / write_output ---- */
-
-/* The block find_longest_match answers for: its bytes, and every position's
- * len | dist << 16 from one launch -- lz4r_block_matches_device for a
- * 300-byte (or shorter) block, lz4r_window_matches_device (the reference's
- * whole 65535-byte window, MAX_MATCH_LENGTH 1024) for a longer block_length.
- * Host and device buffers grow to the block; per thread. */
+/* ---- the match provider of the per-block API (host/compat_lz4.c) ---------
+ * Every position's len | dist << 16 of the n-byte block at `in`, from one
+ * launch: lz4r_block_matches_device for a 300-byte (or shorter) block,
+ * lz4r_window_matches_device (the reference's whole 65535-byte window,
+ * MAX_MATCH_LENGTH 1024) for a longer block_length.  Device buffers grow to
+ * the block; per thread. */
 static __thread struct {
-  const uint8_t *ptr;
-  size_t n, cap;
-  uint8_t *bytes;
-  uint32_t *match;
-  int valid;
+  size_t cap;
   void *d_in, *d_match;
-} fm_cache;
-static __thread size_t fm_block_length;   /* set while block_encode runs */
+} fm_dev;
 
-static void fm_reserve(size_t n) {
-  if (n <= fm_cache.cap) return;
-  free(fm_cache.bytes);
-  free(fm_cache.match);
-  (void)hipFree(fm_cache.d_in);
-  (void)hipFree(fm_cache.d_match);
-  fm_cache.bytes = (uint8_t *)malloc(n);
-  fm_cache.match = (uint32_t *)malloc(n * sizeof(uint32_t));
-  fm_cache.d_in = fm_cache.d_match = NULL;
-  fm_cache.valid = 0;
-  fm_cache.cap = 0;
-  if (!fm_cache.bytes || !fm_cache.match) {
-    perror("Error: Unable to allocate memory");
-    exit(1);
+int lzj_block_matches(const uint8_t *in, size_t n, uint32_t *match) {
+  if (n > fm_dev.cap) {
+    (void)hipFree(fm_dev.d_in);
+    (void)hipFree(fm_dev.d_match);
+    fm_dev.d_in = fm_dev.d_match = NULL;
+    fm_dev.cap = 0;
+    /* +16: the block kernel's staging may read a few bytes past a short block */
+    if (hipMalloc(&fm_dev.d_in, n + 16) != hipSuccess ||
+        hipMalloc(&fm_dev.d_match, n * sizeof(uint32_t)) != hipSuccess)
+      return LZ4R_ERR_NOMEM;
+    fm_dev.cap = n;
   }
-  /* +16: the block kernel's staging may read a few bytes past a short block */
-  if (hipMalloc(&fm_cache.d_in, n + 16) != hipSuccess ||
-      hipMalloc(&fm_cache.d_match, n * sizeof(uint32_t)) != hipSuccess)
-    die_hip("hipMalloc", LZ4R_ERR_NOMEM);
-  fm_cache.cap = n;
-}
-
-static void fm_load(const uint8_t *input, size_t n) {
-  if (fm_cache.valid && fm_cache.ptr == input && fm_cache.n == n &&
-      memcmp(fm_cache.bytes, input, n) == 0)
-    return;
-  fm_reserve(n < LZ4R_BLOCK ? LZ4R_BLOCK : n);
-  int rc = LZ4R_OK;
-  if (hipMemcpy(fm_cache.d_in, input, n, hipMemcpyHostToDevice) != hipSuccess) rc = LZ4R_ERR_HIP;
-  if (rc == LZ4R_OK)
-    rc = n <= LZ4R_BLOCK ? lz4r_block_matches_device(fm_cache.d_in, n, fm_cache.d_match, NULL)
-                         : lz4r_window_matches_device(fm_cache.d_in, n, fm_cache.d_match, NULL);
-  if (rc == LZ4R_OK &&
-      hipMemcpy(fm_cache.match, fm_cache.d_match, n * sizeof(uint32_t), hipMemcpyDeviceToHost) !=
-          hipSuccess)
-    rc = LZ4R_ERR_HIP;
-  if (rc != LZ4R_OK) die_hip("find_longest_match", rc);
-  fm_cache.ptr = input;
-  fm_cache.n = n;
-  memcpy(fm_cache.bytes, input, n);
-  fm_cache.valid = 1;
-}
-
-uint8_t find_longest_match(uint8_t *input, size_t current_index, uint16_t *match_distance) {
-  /* inside block_encode: its block; standalone: the 300 bytes at input */
-  const size_t n = fm_block_length ? fm_block_length : LZ4R_BLOCK;
-  if (current_index >= n) return 0;
-  fm_load(input, n);
-  const uint32_t m = fm_cache.match[current_index];
-  const size_t len = m & 0xFFFFu;
-  if (len < 4) return 0;                               /* MIN_MATCH_LENGTH, LZ4.c:314 */
-  *match_distance = (uint16_t)(m >> 16);
-  return (uint8_t)len;                                 /* uint8_t return, LZ4.c:317 */
-}
-
-static void append_sequence(LZ4Block *block, const LZ4Sequence *q) {   /* LZ4.c:443-459 */
-  LZ4Sequence *s = (LZ4Sequence *)realloc(block->sequences,
-                                          sizeof(LZ4Sequence) * (block->sequences_count + 1));
-  if (!s) {
-    perror("Failed to allocate memory for sequences");
-    exit(EXIT_FAILURE);
-  }
-  block->sequences = s;
-  s[block->sequences_count++] = *q;
-  block->byte_size += q->byte_size;
-}
-
-/* bytes of the literal-length extension as the reference counts them: the
- * remainder is a uint8_t, so (L - 15) & 0xFF == 255 takes two (LZ4.c:554-563) */
-static size_t litext_len(size_t lits) {
-  if (lits < 15) return 0;
-  return ((lits - 15) & 0xFFu) == 255u ? 2 : 1;
-}
-
-void block_encode(const char *block_entry, size_t block_length, LZ4Block *block,
-                  FILE *log_file, FILE *output_file, LZ4Frame *frame) {
-  (void)log_file;
-  (void)output_file;
-  uint8_t *input = (uint8_t *)block_entry;
-  const size_t saved = fm_block_length;
-  fm_block_length = block_length;
-  LZ4Sequence seq = {0};
-  size_t pos = 0;
-  uint16_t lits = 0;
-  while (pos < block_length) {
-    uint16_t dist = 0;
-    const uint8_t m = find_longest_match(input, pos, &dist);
-    if (m == 0) {                                      /* a literal, LZ4.c:522-529 */
-      if (lits == 0) seq.literals = &input[pos];
-      ++pos;
-      ++lits;
-      continue;
-    }
-    /* a match closes the sequence, LZ4.c:533-582.  For m = 1..3 (a 257..259
-     * match truncated to uint8_t) (m - 4) wraps and lands in the token's
-     * high nibble, and the size counts a match-extension byte */
-    const uint8_t tm = m >= 19 ? 15 : (uint8_t)(m - 4);
-    seq.match_offset = dist;
-    seq.literals_count = lits;
-    seq.match_length = m;
-    seq.token = (uint8_t)(((lits >= 15 ? 15 : lits) << 4) | tm);
-    seq.byte_size = (size_t)lits + 5 + litext_len(lits) + ((uint8_t)(m - 4) >= 15 ? 1 : 0);
-    append_sequence(block, &seq);
-    lits = 0;
-    pos += m;
-  }
-  if (lits > 0) {                                      /* literal tail, LZ4.c:585-613 */
-    seq.match_offset = 0;
-    seq.literals_count = lits;
-    seq.match_length = 0;
-    seq.token = (uint8_t)((lits >= 15 ? 15 : lits) << 4);
-    seq.byte_size = (size_t)lits + 5 + litext_len(lits);
-    append_sequence(block, &seq);
-  }
-  block->token = (uint8_t)block->sequences_count;
-  block->byte_size += 3;
-  fm_block_length = saved;
-  /* add_block_to_frame, LZ4.c:461-504 */
-  LZ4Block *fb = (LZ4Block *)realloc(frame->frame_blocks, sizeof(LZ4Block) * (frame->blocks + 1));
-  if (!fb) {
-    perror("Failed to reallocate memory for frame_blocks");
-    exit(EXIT_FAILURE);
-  }
-  frame->frame_blocks = fb;
-  fb[frame->blocks++] = *block;
-}
-
-static void put_u16(FILE *f, size_t v) {
-  const uint8_t b[2] = {(uint8_t)v, (uint8_t)(v >> 8)};   /* low bytes, little endian */
-  fwrite(b, 1, 2, f);
-}
-
-void write_output(LZ4Frame *frame, FILE *out) {
-  const uint8_t nb = (uint8_t)frame->blocks;
-  fwrite(&nb, 1, 1, out);
-  for (size_t i = 0; i < frame->blocks; i++) {
-    const LZ4Block *b = &frame->frame_blocks[i];
-    fwrite(&b->token, 1, 1, out);                     /* write_block, LZ4.c:415-425 */
-    put_u16(out, b->byte_size);
-    for (size_t k = 0; k < b->sequences_count; k++) {
-      const LZ4Sequence *q = &b->sequences[k];        /* write_sequence, LZ4.c:365-413 */
-      fwrite(&q->token, 1, 1, out);
-      put_u16(out, q->byte_size);
-      if (q->literals_count >= 15) {
-        uint8_t r = (uint8_t)(q->literals_count - 15);
-        if (r == 255) {                               /* the uint8_t loop: 255, then 0 */
-          const uint8_t ff = 255;
-          fwrite(&ff, 1, 1, out);
-          r = 0;
-        }
-        fwrite(&r, 1, 1, out);
-      }
-      fwrite(q->literals, 1, q->literals_count, out);
-      put_u16(out, q->match_offset);
-      if (q->match_length >= 4 && (uint8_t)(q->match_length - 4) >= 15) {
-        const uint8_t r = (uint8_t)(q->match_length - 4 - 15);
-        fwrite(&r, 1, 1, out);
-      }
-    }
-    free(b->sequences);
-  }
-  free(frame->frame_blocks);
-  frame->frame_blocks = NULL;
-  frame->blocks = 0;
+  if (hipMemcpy(fm_dev.d_in, in, n, hipMemcpyHostToDevice) != hipSuccess) return LZ4R_ERR_HIP;
+  const int rc = n <= LZ4R_BLOCK ? lz4r_block_matches_device(fm_dev.d_in, n, fm_dev.d_match, NULL)
+                                 : lz4r_window_matches_device(fm_dev.d_in, n, fm_dev.d_match, NULL);
+  if (rc != LZ4R_OK) return rc;
+  if (hipMemcpy(match, fm_dev.d_match, n * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return LZ4R_ERR_HIP;
+  return LZ4R_OK;
 }
 
 void LZ4_decode(char *input_bin_file, char *log) {

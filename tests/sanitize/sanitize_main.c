@@ -11,7 +11,11 @@
  *   - the synthetic generators (host/synth.c, incl. the jump-ahead);
  *   - PNG write / read round trip (host/png_io.c) and a truncated file;
  *   - the JPEG oracle encode / reconstruct and the entropy oracle round
- *     trip on random tiles.
+ *     trip on random tiles;
+ *   - the per-block compat API (host/compat_lz4.c: block_encode,
+ *     write_output, find_longest_match and its growing block cache) over a
+ *     CPU match provider (cpu_matches.c), on 300-B, short and long blocks
+ *     (exact-size heap copies), against the oracle's block encoder.
  * Exit 0 and "sanitize ok" when every check passed.
  */
 #include <stdint.h>
@@ -19,12 +23,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "../../include/lz4jpeg_compat.h"
 #include "../../include/lz4jpeg_synth.h"
 #include "../../include/lz4r.h"
 #include "../../lz4-jpeg_amd/host/lzj_host.h"
 
 size_t lz4o_compress(const uint8_t *in, size_t n, uint8_t *out);
 size_t lz4o_block_bound(void);
+size_t lz4o_encode_block(const uint8_t *blk, size_t n, uint8_t *out);
 size_t lz4o_decompress(const uint8_t *in, size_t in_len, uint8_t *out, size_t cap, size_t nb);
 void jo_encode_image(const uint8_t *rgba, int w, int h, int16_t *out);
 void jo_reconstruct_image(const uint8_t *rgba, int w, int h, uint8_t *out);
@@ -87,6 +93,37 @@ static void lz4_roundtrip(const uint8_t *in, size_t n) {
   free(comp);
 }
 
+/* block_encode + write_output (host/compat_lz4.c) on an exact-size heap copy
+ * of n bytes: the stream must be the frame byte 1 + the oracle's block */
+static void compat_block(const uint8_t *src, size_t n, const char *tmp) {
+  uint8_t *blk = malloc(n);
+  memcpy(blk, src, n);
+  LZ4Frame frame;
+  LZ4Block block;
+  memset(&frame, 0, sizeof frame);
+  memset(&block, 0, sizeof block);
+  block_encode((const char *)blk, n, &block, NULL, NULL, &frame);
+  char path[4096];
+  snprintf(path, sizeof path, "%s/compat_block.bin", tmp);
+  FILE *f = fopen(path, "wb");
+  CHECK(f != NULL);
+  if (!f) {
+    free(blk);
+    return;
+  }
+  write_output(&frame, f);
+  fclose(f);
+  size_t got = 0;
+  uint8_t *bytes = read_file(path, &got);
+  uint8_t *want = malloc(1 + 3 + n + 8 * (n / 4 + 8) + 1024);
+  want[0] = 1;
+  const size_t wl = 1 + lz4o_encode_block(blk, n, want + 1);
+  CHECK(bytes && got == wl && memcmp(bytes, want, wl) == 0);
+  free(want);
+  free(bytes);
+  free(blk);
+}
+
 int main(int argc, char **argv) {
   const char *golden = argc > 1 ? argv[1] : "tests/golden";
   const char *tmp = argc > 2 ? argv[2] : "/tmp";
@@ -111,6 +148,29 @@ int main(int argc, char **argv) {
     lz4_roundtrip(buf, sizeof buf);                       /* no matches */
     for (size_t i = 0; i < sizeof buf; i++) buf[i] = "ab"[(i * 7 / 3) & 1];
     lz4_roundtrip(buf, sizeof buf);
+  }
+
+  /* ---- the per-block compat API over the CPU match provider ---- */
+  if (meta) {
+    compat_block(meta, 300, tmp);
+    compat_block(meta + 300, 57, tmp);                    /* short block */
+    compat_block(meta + 1000, 1000, tmp);                 /* longer: the cache grows */
+    compat_block(meta + 5000, 5000, tmp);
+    compat_block(meta + 2000, 300, tmp);                  /* and shrinks back to 300 B */
+    /* find_longest_match on its own: the 300 bytes at its pointer */
+    uint8_t *b300 = malloc(300);
+    memcpy(b300, meta + 7000, 300);
+    uint32_t *m = malloc(300 * sizeof(uint32_t));
+    lzj_block_matches(b300, 300, m);
+    for (size_t p = 0; p < 300; ++p) {
+      uint16_t d = 0;
+      const uint8_t got = find_longest_match(b300, p, &d);
+      const uint32_t len = m[p] & 0xFFFFu;
+      CHECK(got == (len >= 4 ? (uint8_t)len : 0));
+      CHECK(got == 0 || d == (uint16_t)(m[p] >> 16));
+    }
+    free(m);
+    free(b300);
   }
 
   /* ---- synthetic generators ---- */
