@@ -545,39 +545,53 @@ constexpr size_t kWorkBytesPerLane = 2 * kFullCap /*sym*/ + 2 * kFullCap /*hash*
 
 // ---- decode ------------------------------------------------------------------
 
-// Codes held in LDS per stream (more: regenerated per symbol), sized like
-// the encoder's working set (luma 24, chroma 12): 20 / 10 KB per wave, so a
-// 4K image's 2,025 luma and 4,050 chroma waves each run as ONE round of the
-// chip's wave slots (with 32 codes: 24 / 20 KB, two rounds each)
+// Per stream up to 24 (luma) / 12 (chroma) codes, like the encoder's
+// working set (more: regenerated per symbol, decode_stream_slow): the
+// left-aligned codes in registers, each code's value | length in LDS
+// (14 / 7 KB per wave with the decoded ints, so a 4K image's 2,025 luma and
+// 4,050 chroma waves each run as one round of the chip's wave slots)
 template <int N, int Cap>
 struct DecLds {
-  uint32_t lc[Cap][kLanes];                // left-aligned codes, increasing
-  uint32_t vl[Cap][kLanes];                // value | len << 16
-  alignas(16) int16_t out[kLanes][N];      // the lane's decoded ints (leave as 16-B stores)
+  uint32_t vl[Cap][kLanes];                // value | len << 16 (the codes are in registers)
+  // the lane's decoded ints; rows of N + 2 (an odd number of dwords), so the
+  // lanes' stores at one index hit 64 different banks (rows of N: 32-way)
+  alignas(16) int16_t out[kLanes][N + 2];
 };
 
 // Decode one stream: bits + table -> RLE ints (decode_huffman) -> n ints
 // (inverse_RLE: counts clamped to n, zero fill).  With one code (empty bit
 // string) the reference decodes nothing and keeps its RLE ints: rle_len
 // copies of the symbol.  Returns false on a malformed stream.
-template <typename LcT, typename VlT>
+// The left-aligned codes of a stream with at most Cap codes live in
+// registers (lc[k] for k < U, all ones past U): the symbol at a window is the
+// count of codes <= the window, minus one -- Cap independent compares
+// instead of a binary search whose every step waited on an LDS read.  Only
+// the matched entry's value | length is read from LDS (vl).
+template <int Cap, typename VlT>
 __device__ bool decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
-                              const uint32_t *__restrict__ table, LcT lc, VlT vl,
+                              const uint32_t *__restrict__ table, VlT vl,
                               int16_t *__restrict__ out, int n) {
   const int nbits = (int)(m & 0xFFFF), R = (int)((m >> 16) & 255), U = (int)(m >> 24);
-  if (U == 0 || R == 0 || R > 2 * n) return false;
+  if (U == 0 || U > Cap || R == 0 || R > 2 * n) return false;
   // codes from the lengths, left to right (DFS order)
+  uint32_t lc[Cap];
   uint32_t code = 0;
   int plen = 0;
-  for (int k = 0; k < U; ++k) {
-    const uint32_t e = table[k];
-    const int L = (int)((e >> 16) & 255);
-    if (L > 32 || (U > 1 && L == 0)) return false;
-    if (k) code = L >= plen ? (code + 1) << (L - plen) : (code + 1) >> (plen - L);
-    plen = L;
-    lc[k] = L ? code << (32 - L) : 0;
-    vl[k] = e;
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < Cap; ++k) {
+    lc[k] = ~0u;
+    if (k < U) {
+      const uint32_t e = table[k];
+      const int L = (int)((e >> 16) & 255);
+      bad = bad || L > 32 || (U > 1 && L == 0);
+      if (k) code = L >= plen ? (code + 1) << (L - plen) : (code + 1) >> (plen - L);
+      plen = L;
+      lc[k] = L ? code << (32 - L) : 0;
+      vl[k] = e;
+    }
   }
+  if (bad) return false;
   int idx = 0, pending = -1;                        // pending: a count awaiting its value
   auto put = [&](int v) {
     if (pending < 0) {
@@ -616,14 +630,13 @@ __device__ bool decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
       // 32 bits at p (zero past the end)
       uint32_t win = (uint32_t)(acc >> 32);
       if (nbits - p < 32) win &= ~0u << (32 - (nbits - p));
-      // largest k with lc[k] <= win
-      int lo = 0, hi = U - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (lc[mid] <= win) lo = mid;
-        else hi = mid - 1;
-      }
-      const uint32_t e = vl[lo];
+      // largest k with lc[k] <= win: the codes increase, so it is the count
+      // of codes <= win, minus one (lc[0] = 0; the all-ones entries past U
+      // count only for an all-ones window, whose code is the last)
+      int cnt = 0;
+#pragma unroll
+      for (int k = 0; k < Cap; ++k) cnt += lc[k] <= win ? 1 : 0;
+      const uint32_t e = vl[min(cnt, U) - 1];
       const int L = (int)((e >> 16) & 255);
       if (p + L > nbits || L == 0) return false;
       put((int16_t)(e & 0xFFFF));
@@ -705,15 +718,16 @@ __global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
   // its bits (bits_cap bits) and its table (2 n entries: RLE of n ints)
   const bool sane = (int)(m & 0xFFFF) <= bits_cap(c) && U <= 2 * n;
   const bool ok = sane && (U <= Cap
-                               ? decode_stream(b, m, t, Col<uint32_t>{&S.lc[0][lane], kLanes},
-                                               Col<uint32_t>{&S.vl[0][lane], kLanes}, o, n)
+                               ? decode_stream<Cap>(b, m, t, Col<uint32_t>{&S.vl[0][lane], kLanes},
+                                                    o, n)
                                : decode_stream_slow(b, m, t, o, n));
   if (!sane)
     for (int j = 0; j < n; ++j) o[j] = 0;
   if (!ok) atomicAdd(&status[1], 1u);
   uint4 *dst = reinterpret_cast<uint4 *>(coef + tile * 128 + coef_off(c));
-  const uint4 *src = reinterpret_cast<const uint4 *>(o);
-  for (int v = 0; v < n / 8; ++v) dst[v] = src[v];
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(o);    // 4-B aligned rows
+  for (int v = 0; v < n / 8; ++v)
+    dst[v] = make_uint4(src[4 * v], src[4 * v + 1], src[4 * v + 2], src[4 * v + 3]);
 }
 
 __global__ void entropy_init(ScratchHdr *hdr, uint32_t *status) {
