@@ -54,6 +54,23 @@ __device__ __forceinline__ int clamp_u8(int v) {       // JPEG.c:132-139
 // One pixel's contribution to the tile planes (JPEG.c:127, 157, 180;
 // chroma only from odd columns: chroma_subsample JPEG.c:329-331 +
 // divide_image JPEG.c:540-544).  `valid` = inside the image.
+//
+// The reference evaluates Y = (uint8_t)((0.299 R + 0.587 G) + 0.114 B) and
+// Cr / Cb = clamp((int)(... + 128.0)) in fp64.  With N = 299 R + 587 G + 114 B
+// (Cr: 439 R - 368 G - 71 B + 128000, Cb: -148 R - 291 G + 439 B + 128000;
+// all positive), the fp64 value lies within 1e-13 of N / 1000 (three
+// roundings of the constants, three of the products, three or four of the
+// sums, each far below 2^-43 at these magnitudes), so its truncation is
+// floor(N / 1000) whenever N is not a multiple of 1000 (the fraction is then
+// in [0.001, 0.999]).  Those lanes take the integer path: N by 24-bit
+// multiply-adds, the quotient by one v_mul_hi_u32_u24 with ceil(2^32 / 1000)
+// (exact for N < 2^18), the remainder by one multiply-add.  A lane whose N is
+// a multiple of 1000 (about 1 in 1000) evaluates the reference's fp64
+// expression, behind a branch taken only when some lane needs it.
+__device__ __forceinline__ uint32_t div1000(uint32_t N) {       // N < 2^18
+  return (uint32_t)(((uint64_t)N * 4294968u) >> 32);
+}
+
 __device__ __forceinline__ void convert_pixel(uint32_t p, bool valid, int r,
                                               int px, double *ylds,
                                               double *crl, double *cbl) {
@@ -61,17 +78,29 @@ __device__ __forceinline__ void convert_pixel(uint32_t p, bool valid, int r,
   const unsigned R = p & 255u, G = (p >> 8) & 255u, B = (p >> 16) & 255u;
   int yv = 0;
   if (valid) {
-    double y = 0.299 * (double)R + 0.587 * (double)G + 0.114 * (double)B;
-    yv = (int)(uint8_t)(unsigned)y;            // (uint8_t) of a double in [0,256)
+    const uint32_t N = 299u * R + 587u * G + 114u * B;
+    const uint32_t q = div1000(N);
+    yv = (int)q;
+    if (N == 1000u * q) {                      // on an integer: the reference's fp64
+      double y = 0.299 * (double)R + 0.587 * (double)G + 0.114 * (double)B;
+      yv = (int)(uint8_t)(unsigned)y;          // (uint8_t) of a double in [0,256)
+    }
   }
   ylds[tile * kYStride + r * 8 + col] = (double)(yv - 128);   // JPEG.c:467
   if (col & 1) {
     int crv = 0, cbv = 0;
     if (valid) {
-      crv = clamp_u8((int)(0.439 * (double)R - 0.368 * (double)G -
-                           0.071 * (double)B + 128.0));
-      cbv = clamp_u8((int)(-0.148 * (double)R - 0.291 * (double)G +
-                           0.439 * (double)B + 128.0));
+      const uint32_t Nr = 128000u + 439u * R - 368u * G - 71u * B;   // > 0
+      const uint32_t Nb = 128000u + 439u * B - 148u * R - 291u * G;  // > 0
+      const uint32_t qr = div1000(Nr), qb = div1000(Nb);
+      crv = clamp_u8((int)qr);
+      cbv = clamp_u8((int)qb);
+      if (Nr == 1000u * qr)
+        crv = clamp_u8((int)(0.439 * (double)R - 0.368 * (double)G -
+                             0.071 * (double)B + 128.0));
+      if (Nb == 1000u * qb)
+        cbv = clamp_u8((int)(-0.148 * (double)R - 0.291 * (double)G +
+                             0.439 * (double)B + 128.0));
     }
     const int ci = tile * kCStride + r * 4 + (col >> 1);
     crl[ci] = (double)(crv - 128);
