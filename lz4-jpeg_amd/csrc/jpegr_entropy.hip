@@ -79,19 +79,25 @@ struct Col {
 // conflicts under divergent indices).
 template <typename T>
 struct LCol {
+  // Every access is type-punned over u32 storage (elements of 1, 2 or 4
+  // bytes, pairs read as one dword): may_alias, or type-based alias analysis
+  // lets the compiler move a dword read above a half-word store of the same
+  // word (it did, once a sift was unrolled without branches).
+  typedef T __attribute__((may_alias)) TA;
+  typedef uint32_t __attribute__((may_alias)) WA;
   uint8_t *p;                                   // &block[0][lane] as bytes
-  __device__ __forceinline__ T &operator[](int i) const {
+  __device__ __forceinline__ TA &operator[](int i) const {
     constexpr int per = 4 / (int)sizeof(T);
-    return *reinterpret_cast<T *>(p + (i / per) * (4 * kLanes) + (i % per) * (int)sizeof(T));
+    return *reinterpret_cast<TA *>(p + (i / per) * (4 * kLanes) + (i % per) * (int)sizeof(T));
   }
   // zero elements [0, n) (n a multiple of 4 / sizeof(T)): whole dwords
   __device__ __forceinline__ void clear(int n) const {
     constexpr int per = 4 / (int)sizeof(T);
-    for (int i = 0; i < n / per; ++i) *reinterpret_cast<uint32_t *>(p + i * (4 * kLanes)) = 0u;
+    for (int i = 0; i < n / per; ++i) *reinterpret_cast<WA *>(p + i * (4 * kLanes)) = 0u;
   }
   // 16-bit elements i, i + 1 (i even: one dword, one LDS read)
   __device__ __forceinline__ uint32_t pair(int i) const {
-    return *reinterpret_cast<const uint32_t *>(p + (i / 2) * (4 * kLanes));
+    return *reinterpret_cast<const WA *>(p + (i / 2) * (4 * kLanes));
   }
 };
 
@@ -153,6 +159,60 @@ __device__ __forceinline__ uint16_t sift(const W &w, int size, int i, uint16_t x
   return top;
 }
 
+// The same sift for heaps of at most Cap <= 32 entries, branch-free: a fixed
+// floor(log2(Cap)) levels (the deepest any sift can go), two per LDS round
+// trip, a done flag instead of a break.  Once x has landed, the remaining
+// levels rewrite x at its index (idempotent).  The loop form above paid the
+// exec-mask bookkeeping of every lane's own exit at every level.
+template <int Cap, class W>
+__device__ __forceinline__ uint16_t sift_fixed(const W &w, int size, int i, uint16_t x) {
+  constexpr int kMaxSlot = Cap & ~1;
+  constexpr int kDepth = Cap >= 16 ? 4 : Cap >= 8 ? 3 : Cap >= 4 ? 2 : 1;   // floor(log2 Cap)
+  static_assert(Cap <= 31, "fixed depth");
+  const int cx = x >> 8;
+  uint16_t top = x;
+  bool done = false;
+#pragma unroll
+  for (int d = 0; d < kDepth; d += 2) {
+    const int l = 2 * i + 1, r = l + 1;
+    const uint32_t pc = w.heap.pair(min(l + 1, kMaxSlot));      // entries l, r
+    const uint32_t pgl = w.heap.pair(min(2 * l + 2, kMaxSlot));  // l's children
+    const uint32_t pgr = w.heap.pair(min(2 * l + 4, kMaxSlot));  // r's children
+    {
+      const uint16_t hl = (uint16_t)pc, hr = (uint16_t)(pc >> 16);
+      const bool tl = l < size && (hl >> 8) < cx;
+      const int cs = tl ? (hl >> 8) : cx;
+      const bool tr = r < size && (hr >> 8) < cs;
+      const bool mv = !done && (tl || tr);
+      const uint16_t hs = tr ? hr : hl;
+      if (d == 0) top = mv ? hs : x;
+      w.heap[i + 1] = mv ? hs : x;
+      done = !mv;
+      i = mv ? (tr ? r : l) : i;
+    }
+    if (d + 1 < kDepth) {
+      const uint32_t pg = i == r ? pgr : pgl;                 // (unused once done)
+      const int l2 = 2 * i + 1, r2 = l2 + 1;
+      const uint16_t gl = (uint16_t)pg, gr = (uint16_t)(pg >> 16);
+      const bool tl = l2 < size && (gl >> 8) < cx;
+      const int cs = tl ? (gl >> 8) : cx;
+      const bool tr = r2 < size && (gr >> 8) < cs;
+      const bool mv = !done && (tl || tr);
+      w.heap[i + 1] = mv ? (tr ? gr : gl) : x;
+      done = !mv;
+      i = mv ? (tr ? r2 : l2) : i;
+    }
+  }
+  w.heap[i + 1] = x;
+  return top;
+}
+
+template <int Cap, class W>
+__device__ __forceinline__ uint16_t sift_any(const W &w, int size, int i, uint16_t x) {
+  if constexpr (Cap <= 31) return sift_fixed<Cap>(w, size, i, x);
+  else return sift<Cap & ~1>(w, size, i, x);
+}
+
 // The Huffman code of one stream from its U symbols' counts, exactly as the
 // reference builds it: build_heap (JPEG.c:913-936) over the frequency list in
 // first-occurrence order, build_huffman_tree (:938-962: pop, pop, append the
@@ -162,8 +222,7 @@ __device__ __forceinline__ uint16_t sift(const W &w, int size, int i, uint16_t x
 // order).  Returns true when a code exceeds the reference's char code[32].
 template <int Cap, class W>
 __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
-  constexpr int kMaxSlot = Cap & ~1;                  // heap slots 0 .. Cap + 1
-  for (int i = U / 2 - 1; i >= 0; --i) sift<kMaxSlot>(w, U, i, w.heap[i + 1]);
+  for (int i = U / 2 - 1; i >= 0; --i) sift_any<Cap>(w, U, i, w.heap[i + 1]);
   int size = U, next = U;
   uint16_t root = w.heap[1];
   while (size > 1) {
@@ -171,10 +230,10 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
     // known in registers), append the merged node unsifted
     const uint16_t left = root;
     --size;
-    root = sift<kMaxSlot>(w, size, 0, w.heap[size + 1]);
+    root = sift_any<Cap>(w, size, 0, w.heap[size + 1]);
     const uint16_t right = root;
     --size;
-    root = sift<kMaxSlot>(w, size, 0, w.heap[size + 1]);
+    root = sift_any<Cap>(w, size, 0, w.heap[size + 1]);
     const uint16_t merged = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next);
     w.heap[size + 1] = merged;                                              // not sifted up
     w.heap[U - (next - U)] = (uint16_t)((left & 255) | ((right & 255) << 8));   // freed slot
