@@ -13,7 +13,7 @@ CSRC    := $(PKG)/csrc
 HOST    := $(PKG)/host
 B       := $(PKG)/build
 BIN     := $(PKG)/bin
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -ffp-contract=off -fPIC -std=c++17 -Wall \
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -ffp-contract=off -fno-strict-aliasing -fPIC -std=c++17 -Wall \
             -Wno-unused-result
 CFLAGS_HOST := -O2 -fPIC -Wall -std=gnu11 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
 LIB     := $(PKG)/lz4jpeg/liblz4jpeg.so

@@ -9,7 +9,7 @@ obj=${3:-lz4r}
 case $obj in lz4r) lib=liblz4_$2.so ;; jpegr) lib=libjpeg_$2.so ;; *) lib=lib${obj}_$2.so ;; esac
 mkdir -p tools/variants
 cp "$1" tools/variants/${obj}_$2.hip
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -std=c++17 $EXTRA \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-strict-aliasing -fPIC -std=c++17 $EXTRA \
   -I include -I lz4-jpeg_amd/csrc -c tools/variants/${obj}_$2.hip -o tools/variants/${obj}_$2.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/variants/$lib \
   tools/variants/${obj}_$2.o $(ls lz4-jpeg_amd/build/*.o | grep -v -e "/$obj.o" -e _seq.o -e _par.o -e png_io.o)
