@@ -1027,8 +1027,10 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   static_assert(kGH * kPerSlot <= 64 * kEW, "one record load per thread");
   uint4 rv = make_uint4(0, 0, 0, 0);
   const int rhb = tid / kPerSlot, rj = tid % kPerSlot;
+  // the workgroup's slots: a uniform base and 32-bit offsets
+  const uint8_t *const wslots = slots + (b0 - slot_base) * (size_t)kSlot;
   if (tid < (h1 - h0) * kPerSlot)
-    rv = reinterpret_cast<const uint4 *>(slots + (b0 + rhb - slot_base) * (size_t)kSlot)[rj];
+    rv = reinterpret_cast<const uint4 *>(wslots + rhb * kSlot)[rj];
   constexpr int kSt16 = (kGH * kBlk) / 16;         // 600 16-B chunks of staged input
   constexpr int kStPer = (kSt16 + 64 * kEW - 1) / (64 * kEW);
   uint4 sv[kStPer];
@@ -1081,7 +1083,11 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
 #pragma unroll
       for (int i = 0; i < kBW; ++i)
         st[i] = i < nbk ? __builtin_amdgcn_readlane(sst, i) : 0x7fffffff;
-      int end_prev = 0, cont = 0;
+      // the wave's blocks are contiguous in the image, each its 3 header bytes
+      // and then its sequences' bytes (tsz counts the bytes written): sequence f
+      // lands at the wave's first image byte + 3 (its block's rank + 1) + the
+      // bytes of the wave's sequences before it
+      int end_prev = 0, wcur = lead + (int)(toff[bl0] - G0) + 3;
       for (int f0 = 0; f0 < Stot; f0 += 64) {
         const int f = f0 + lane;
         const bool valid = f < Stot;
@@ -1094,9 +1100,7 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
         }
         const int k = f - sb;                      // sequence index in the block
         const int hb = bl0 + bi;
-        const size_t tb = g0 + hb;                 // block index of the call
-        const uint32_t *rp =
-            reinterpret_cast<const uint32_t *>(slots + (tb - slot_base) * (size_t)kSlot);
+        const uint32_t *rp = reinterpret_cast<const uint32_t *>(wslots + (hb - h0) * kSlot);
         const uint32_t r = !valid ? 0u : (1 + k < kRecPre ? recst[hb - h0][1 + k] : rp[1 + k]);
         const int cpos = (int)(r & 511u);
         const int M = (int)((r >> 9) & 255u), D = (int)(r >> 17);
@@ -1111,15 +1115,8 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
         const bool mextW = M >= 4 && mx >= 15, mextS = M != 0 && mx >= 15;
         const int bytes = valid ? 5 + le + L + (mextW ? 1 : 0) : 0;
         const uint32_t inc = wave_incl_add((uint32_t)bytes);
-        // offsets restart at every block; the round's first block may continue
-        // one that began in an earlier round (it then starts at `cont`)
-        // (the cross-lane read stays outside any select: in a divergent region
-        // ds_bpermute would read 0 from the lanes the select turned off)
-        const int incb = __shfl((int)inc, max(sb - f0 - 1, 0), 64);
-        const int segb = sb > f0 ? incb : 0;
-        const int orel = 3 + (int)inc - bytes - segb + (sb < f0 ? cont : 0);
-        const int ib = lead + (int)(toff[hb] - G0);                  // block's first image byte
-        const int o = ib + orel;
+        const int o = wcur + 3 * bi + (int)inc - bytes;               // the sequence's token
+        const int ib = o - 3;                                         // (k == 0) its block's header
         const int ol = o + 3 + le;                                   // first literal byte
         if (valid) {
           const int tl = L >= 15 ? 15 : L;                            // LZ4.c:540
@@ -1140,7 +1137,12 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
           const int cw = valid && L > 0 ? ((ol + L - 1) >> 3) - (ol >> 3) + 1 : 0;
           const uint32_t cinc = wave_incl_add((uint32_t)cw);
           const int C = (int)lane63(cinc), stw = (int)dpp<0x138, 0xf, 0xf>(cinc);
-          const int lsrc = (L << 16) | (kStagePad + kBlk * (hb - h0) + pend);
+          // the run, as its owning lanes use it: image word w = (ol >> 3) - stw + gw,
+          // stage byte of that word's first image byte xs = 8 w + (src - ol), and
+          // its bytes [ol, ol + L) of the image (two 16-bit fields per dword)
+          const int src = kStagePad + kBlk * (hb - h0) + pend;
+          const uint32_t rw = ((uint32_t)((ol >> 3) - stw) & 0xFFFFu) | ((uint32_t)(src - ol) << 16);
+          const uint32_t rb = (uint32_t)ol | ((uint32_t)(ol + L) << 16);
           uint32_t carry = 0;                    // 1 + the last run owning a word so far
           for (int w0 = 0; w0 < C; w0 += 64) {
             wave_sync();
@@ -1151,25 +1153,25 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
             carry = lane63(k1);
             const int gw = w0 + lane;
             const int kr = ((int)k1 - 1) & 63;   // the run owning word gw
-            const int kol = __shfl(ol, kr, 64);
-            const int kls = __shfl(lsrc, kr, 64);
-            const int sk = __shfl(stw, kr, 64);
+            const uint32_t kw = (uint32_t)__shfl((int)rw, kr, 64);
+            const uint32_t kb = (uint32_t)__shfl((int)rb, kr, 64);
             if (gw < C) {
-              const int kL = kls >> 16, ksrc = kls & 0xFFFF;
-              const int w = (kol >> 3) + (gw - sk);                   // image word
-              const int xs = 8 * w + ksrc - kol;                       // its input bytes
+              const int t = 8 * ((int)(int16_t)(kw & 0xFFFFu) + gw);   // image word's first byte
+              const int xs = t + ((int)kw >> 16);                      // its input bytes
               const uint64_t *iw = reinterpret_cast<const uint64_t *>(stage + (xs & ~7));
               const uint64_t lo = iw[0], hi = iw[1];
               const uint32_t sh = 8u * (uint32_t)(xs & 7);
-              const uint64_t v = (lo >> sh) | ((hi << 1) << (63u - sh));
-              const int lb = max(kol - 8 * w, 0), hbb = min(kol + kL - 8 * w, 8);
-              const uint64_t mask = (~0ull << (8 * lb)) & (~0ull >> (64 - 8 * hbb));
-              atomicOr(reinterpret_cast<unsigned long long *>(img + 8 * w),
-                       (unsigned long long)(v & mask));
+              uint64_t v = (lo >> sh) | ((hi << 1) << (63u - sh));
+              // keep the run's bytes [lb, hb) of the word: shift the others out
+              const uint32_t l8 = 8u * (uint32_t)max((int)(kb & 0xFFFFu) - t, 0);
+              const uint32_t h8 = 64u - 8u * (uint32_t)min((int)(kb >> 16) - t, 8);
+              v = (v >> l8) << l8;
+              v = (v << h8) >> h8;
+              atomicOr(reinterpret_cast<unsigned long long *>(img + t), (unsigned long long)v);
             }
           }
         }
-        cont = (int)lane63((uint32_t)(orel + bytes - 3));  // bytes of lane 63's block so far
+        wcur += (int)lane63(inc);
       }
     }
   }
@@ -1178,24 +1180,23 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   const uint64_t G1 = min(toff[h1], cap);
   if (G1 <= G0) return;
   // chunk ci covers stream bytes [F + 16 ci, F + 16 ci + 16), F = G0 - lead
-  // (16-B aligned): offsets from `out`, so the stores stay global_store (a
-  // pointer rebuilt from an integer is a flat address: every flat store also
-  // counts in lgkmcnt and serialised this loop behind its LDS reads)
+  // (16-B aligned), as 32-bit offsets (the range is at most kEmitImg bytes) from
+  // out + F, so the stores stay global_store (a pointer rebuilt from an integer
+  // is a flat address: every flat store also counts in lgkmcnt and serialised
+  // this loop behind its LDS reads)
   const uint64_t F = G0 - (uint64_t)lead;
-  const int nchunks = (int)((G1 - F + 15) >> 4);
-  for (int ci = tid; ci < nchunks; ci += 64 * kEW) {
-    const uint64_t a = F + ((uint64_t)ci << 4);
-    const uint4 v = reinterpret_cast<const uint4 *>(img)[ci];
-    if (a >= G0 && a + 16 <= G1) {
-      *reinterpret_cast<uint4 *>(out + a) = v;
-    } else {
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        const uint64_t ab = a + b;
-        if (ab >= G0 && ab < G1) out[ab] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-      }
-    }
+  uint8_t *const outF = out + F;
+  const uint32_t nrel = (uint32_t)(G1 - F);
+  const uint32_t c0 = lead ? 1u : 0u, c1 = nrel >> 4;   // the whole chunks: [c0, c1)
+  for (uint32_t ci = c0 + (uint32_t)tid; ci < c1; ci += 64 * kEW)
+    *reinterpret_cast<uint4 *>(outF + 16u * ci) = reinterpret_cast<const uint4 *>(img)[ci];
+  // the partial chunks at either end, a byte per lane: lanes 0-15 the first
+  // chunk's bytes [lead, 16), lanes 16-31 the last one's [16 c1, nrel) (when it
+  // is not the first)
+  if (wv == kEW - 1 && lane < 32) {
+    const uint32_t x = lane < 16 ? (uint32_t)lane : 16u * c1 + (uint32_t)(lane - 16);
+    const bool own = lane < 16 ? (c0 && x >= (uint32_t)lead && x < nrel) : (c1 >= c0 && x < nrel);
+    if (own) outF[x] = img[x];
   }
 }
 
