@@ -894,30 +894,48 @@ __global__ __launch_bounds__(256) void lz4_window_matches(const uint8_t *__restr
 constexpr int kGT = 64;              // tiles per gather group (one workgroup)
 constexpr int kPart = 64 * kGT;      // tiles per scan partial (64 groups)
 
-// per group of 64 tiles: gsum; per 64 groups: part
+// per group of 64 tiles: gsum; per 64 groups: part.  Coalesced: load k of
+// the workgroup reads tiles [1024 k, 1024 k + 1024) of the partial as uint4,
+// 16 lanes (one DPP row) per group of 64 tiles.
 __global__ __launch_bounds__(256) void lz4_scan_reduce(const uint32_t *__restrict__ tsz,
                                                        size_t ntiles, size_t p_first,
                                                        uint32_t *__restrict__ gsum,
                                                        uint64_t *__restrict__ part) {
-  __shared__ uint64_t ws[4];
+  __shared__ uint32_t ws[4];
   const int tid = threadIdx.x;
   const size_t pi = p_first + blockIdx.x;                            // partial index
-  const size_t t0 = pi * kPart + (size_t)tid * 16;                   // 16 tiles per thread
-  uint32_t v = 0;
+  const size_t q0 = pi * (kPart / 4);                                // its first uint4
+  uint32_t v[4];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const size_t i = t0 + k;
-    if (i < ntiles) v += tsz[i];
+  for (int k = 0; k < 4; ++k) {
+    const size_t q = q0 + (size_t)(256 * k + tid);                   // tiles 4q .. 4q + 3
+    if (4 * q + 4 <= ntiles) {
+      const uint4 x = reinterpret_cast<const uint4 *>(tsz)[q];
+      v[k] = x.x + x.y + x.z + x.w;
+    } else {
+      v[k] = 0;
+      for (int j = 0; j < 4; ++j)
+        if (4 * q + j < ntiles) v[k] += tsz[4 * q + j];
+    }
   }
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);                      // 4 threads = one group of 64 tiles
-  const size_t g = pi * 64 + (tid >> 2);
-  if ((tid & 3) == 0 && g * kGT < ntiles) gsum[g] = v;
-  uint64_t w = (tid & 3) == 0 ? v : 0;
-  w = wave_sum64(w);
-  if ((tid & 63) == 0) ws[tid >> 6] = w;
+  uint32_t tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t x = v[k];                       // row prefix: lane 15 of the row holds the group
+    x += dpp<0x111, 0xf, 0xf>(x);
+    x += dpp<0x112, 0xf, 0xf>(x);
+    x += dpp<0x114, 0xf, 0xf>(x);
+    x += dpp<0x118, 0xf, 0xf>(x);
+    const size_t g = pi * 64 + (size_t)(16 * k + (tid >> 4));
+    if ((tid & 15) == 15) {
+      if (g * kGT < ntiles) gsum[g] = x;
+      tot += x;
+    }
+  }
+  tot = wave_incl_add(tot);                  // < 2^32: 4096 tiles of <= 548 B
+  if ((tid & 63) == 63) ws[tid >> 6] = tot;
   __syncthreads();
-  if (tid == 0) part[pi] = ws[0] + ws[1] + ws[2] + ws[3];
+  if (tid == 0) part[pi] = (uint64_t)ws[0] + ws[1] + ws[2] + ws[3];
 }
 
 // one workgroup: exclusive scan of the partials in place, as absolute stream
