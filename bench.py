@@ -361,20 +361,25 @@ def run_lz4(ctx, n_total, scaling):
         ldist.exchange_lengths(seg, dev)
         return seg
 
+    # the per-call timing events are created and first recorded in the warm-up
+    # steps (their one-off cost would otherwise land in the first timed step)
+    comp.set_timing(True)
     for _ in range(args.warmup):
         out_len = lz4_step()
     if out_len > cap:
         raise RuntimeError(f"lz4: output {out_len} B exceeds the bench buffer {cap} B")
     torch.cuda.synchronize()
     ctx.barrier()
-    comp.set_timing(True)
     match_ms, call_ms = [], []
     torch.cuda.synchronize()
     ctx.barrier()
+    step_ms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        ts = time.perf_counter()
         out_len = lz4_step()
         c_ms, m_ms = comp.last_timing()
+        step_ms.append((time.perf_counter() - ts) * 1e3)
         call_ms.append(c_ms)
         match_ms.append(m_ms)
     torch.cuda.synchronize()
@@ -387,7 +392,9 @@ def run_lz4(ctx, n_total, scaling):
     avg_call_ms = ctx.max_over_ranks(sum(call_ms) / len(call_ms))
     out_total = ctx.sum_over_ranks(out_len) + (1 if world > 1 else 0)
     log(f"lz4: {lz4_ms:.3f} ms/step, {lz4_gbs:.1f} GB/s aggregate, lz4_tiles "
-        f"{avg_match_ms:.3f} ms, call {avg_call_ms:.3f} ms, out {out_total} B")
+        f"{avg_match_ms:.3f} ms, call {avg_call_ms:.3f} ms, out {out_total} B; step wall "
+        f"min/median/max {min(step_ms):.3f}/{sorted(step_ms)[len(step_ms) // 2]:.3f}/"
+        f"{max(step_ms):.3f} ms")
 
     # decoder: this rank's blocks -> bytes, in HBM, with the
     # compressor's device-resident block offsets (no host round trip)
@@ -559,13 +566,13 @@ def run_cfg4_share(ctx, comp):
         comp.compress_async(d_in, n, d_out, d_len, segment=True, final_shard=False)
         return int(d_len.item())
 
+    comp.set_timing(True)                  # events made in the warm-up (two chunks here)
     for _ in range(max(1, args.warmup)):
         seg = step()
     if seg > cap:
         raise RuntimeError(f"lz4 cfg4 share: segment {seg} B exceeds {cap} B")
     torch.cuda.synchronize()
     warm = max(1, args.warmup) + settle(step, torch.cuda.synchronize, chunk=1)
-    comp.set_timing(True)
     tiles = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
