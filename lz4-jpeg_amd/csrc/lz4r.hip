@@ -81,7 +81,8 @@
 // (the Makefile's product build never defines it): 1 = no match search,
 // 2 = no index/match phase, 3 = index only (no candidates), 4 = candidates
 // without the lcp verification, 5 = the lcp without its result (no
-// matches downstream), 11 = no sequence emission.
+// matches downstream), 11 = no sequence emission; lz4_emit: 31 = no literal
+// words, 32 = no header bytes.
 #ifndef LZ4R_VARIANT
 #define LZ4R_VARIANT 0
 #endif
@@ -1136,7 +1137,7 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
         const int o = wcur + 3 * bi + (int)inc - bytes;               // the sequence's token
         const int ib = o - 3;                                         // (k == 0) its block's header
         const int ol = o + 3 + le;                                   // first literal byte
-        if (valid) {
+        if (valid && LZ4R_VARIANT != 32) {                            // (32: tools ablation)
           const int tl = L >= 15 ? 15 : L;                            // LZ4.c:540
           const int tm = M == 0 ? 0 : (M >= 19 ? 15 : mx);            // LZ4.c:542
           const uint32_t ext = le == 0 ? 0u : (rem == 255 ? 255u : (uint32_t)rem);
@@ -1154,7 +1155,8 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
         {
           const int cw = valid && L > 0 ? ((ol + L - 1) >> 3) - (ol >> 3) + 1 : 0;
           const uint32_t cinc = wave_incl_add((uint32_t)cw);
-          const int C = (int)lane63(cinc), stw = (int)dpp<0x138, 0xf, 0xf>(cinc);
+          const int C = LZ4R_VARIANT == 31 ? 0 : (int)lane63(cinc);   // (31: tools ablation)
+          const int stw = (int)dpp<0x138, 0xf, 0xf>(cinc);
           // the run, as its owning lanes use it: image word w = (ol >> 3) - stw + gw,
           // stage byte of that word's first image byte xs = 8 w + (src - ol), and
           // its bytes [ol, ol + L) of the image (two 16-bit fields per dword)
