@@ -44,6 +44,148 @@ __global__ __launch_bounds__(64) void body(uint32_t *out, uint64_t *clk) {
           "v_mul_lo_u32 %3, %3, %0\n\tv_mul_lo_u32 %0, %0, %2\n\tv_mul_lo_u32 %1, %1, %3\n\t"
           "v_mul_lo_u32 %2, %2, %0\n\tv_mul_lo_u32 %3, %3, %1\n\t"
           : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 5) {  // 8 v_lshlrev_b64 (4 chains of 64-bit pairs)
+      uint64_t x = ((uint64_t)a << 32) | b, y = ((uint64_t)c << 32) | d;
+      asm volatile(
+          "v_lshlrev_b64 %0, %2, %0\n\tv_lshrrev_b64 %1, %3, %1\n\t"
+          "v_lshlrev_b64 %0, %3, %0\n\tv_lshrrev_b64 %1, %2, %1\n\t"
+          "v_lshlrev_b64 %0, %2, %0\n\tv_lshrrev_b64 %1, %3, %1\n\t"
+          "v_lshlrev_b64 %0, %3, %0\n\tv_lshrrev_b64 %1, %2, %1\n\t"
+          : "+v"(x), "+v"(y) : "v"(a & 7u), "v"(c & 7u));
+      a = (uint32_t)x; b = (uint32_t)(x >> 32); c = (uint32_t)y; d = (uint32_t)(y >> 32);
+    } else if (KIND == 6) {  // 8 v_alignbyte_b32
+      asm volatile(
+          "v_alignbyte_b32 %0, %1, %0, %2\n\tv_alignbyte_b32 %1, %2, %1, %3\n\t"
+          "v_alignbyte_b32 %2, %3, %2, %0\n\tv_alignbyte_b32 %3, %0, %3, %1\n\t"
+          "v_alignbyte_b32 %0, %1, %0, %2\n\tv_alignbyte_b32 %1, %2, %1, %3\n\t"
+          "v_alignbyte_b32 %2, %3, %2, %0\n\tv_alignbyte_b32 %3, %0, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 7) {  // 8 v_cndmask_b32 on vcc-free SGPR masks
+      asm volatile(
+          "v_cndmask_b32_e64 %0, %0, %1, %4\n\tv_cndmask_b32_e64 %1, %1, %2, %5\n\t"
+          "v_cndmask_b32_e64 %2, %2, %3, %4\n\tv_cndmask_b32_e64 %3, %3, %0, %5\n\t"
+          "v_cndmask_b32_e64 %0, %0, %1, %5\n\tv_cndmask_b32_e64 %1, %1, %2, %4\n\t"
+          "v_cndmask_b32_e64 %2, %2, %3, %5\n\tv_cndmask_b32_e64 %3, %3, %0, %4\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d)
+          : "s"((uint64_t)s0 * 0x9E3779B97F4A7C15ull), "s"((uint64_t)s1 * 0xC2B2AE3D27D4EB4Full));
+    } else if (KIND == 8) {  // 8 v_add3_u32 / v_lshl_add_u32 (VOP3 three-operand)
+      asm volatile(
+          "v_add3_u32 %0, %0, %1, %2\n\tv_lshl_add_u32 %1, %1, 2, %2\n\t"
+          "v_add3_u32 %2, %2, %3, %0\n\tv_lshl_add_u32 %3, %3, 3, %0\n\t"
+          "v_add3_u32 %0, %0, %1, %2\n\tv_lshl_add_u32 %1, %1, 2, %3\n\t"
+          "v_add3_u32 %2, %2, %3, %1\n\tv_lshl_add_u32 %3, %3, 3, %2\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 9) {  // 8 v_mbcnt_lo/hi
+      asm volatile(
+          "v_mbcnt_lo_u32_b32 %0, %4, %0\n\tv_mbcnt_hi_u32_b32 %1, %4, %1\n\t"
+          "v_mbcnt_lo_u32_b32 %2, %4, %2\n\tv_mbcnt_hi_u32_b32 %3, %4, %3\n\t"
+          "v_mbcnt_lo_u32_b32 %0, %4, %0\n\tv_mbcnt_hi_u32_b32 %1, %4, %1\n\t"
+          "v_mbcnt_lo_u32_b32 %2, %4, %2\n\tv_mbcnt_hi_u32_b32 %3, %4, %3\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "s"(s0));
+    } else if (KIND == 10) { // 8 v_perm_b32
+      asm volatile(
+          "v_perm_b32 %0, %1, %0, %4\n\tv_perm_b32 %1, %2, %1, %4\n\t"
+          "v_perm_b32 %2, %3, %2, %4\n\tv_perm_b32 %3, %0, %3, %4\n\t"
+          "v_perm_b32 %0, %1, %0, %4\n\tv_perm_b32 %1, %2, %1, %4\n\t"
+          "v_perm_b32 %2, %3, %2, %4\n\tv_perm_b32 %3, %0, %3, %4\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "s"(0x05040100u));
+    } else if (KIND == 11) { // 8 v_mov_b32_dpp wave_shr:1
+      asm volatile(
+          "v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mov_b32_dpp %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mov_b32_dpp %2, %3 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mov_b32_dpp %3, %0 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mov_b32_dpp %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mov_b32_dpp %2, %3 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mov_b32_dpp %3, %0 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 12) { // 8 v_bfe_u32 / v_and_or_b32
+      asm volatile(
+          "v_bfe_u32 %0, %1, 3, 9\n\tv_and_or_b32 %1, %2, %0, %3\n\t"
+          "v_bfe_u32 %2, %3, 5, 7\n\tv_and_or_b32 %3, %0, %2, %1\n\t"
+          "v_bfe_u32 %0, %1, 3, 9\n\tv_and_or_b32 %1, %2, %0, %3\n\t"
+          "v_bfe_u32 %2, %3, 5, 7\n\tv_and_or_b32 %3, %0, %2, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 13) { // 8 v_cmp_lt_u32 -> SGPR pairs
+      uint64_t m0 = 0, m1 = 0;
+      asm volatile(
+          "v_cmp_lt_u32_e64 %4, %0, %1\n\tv_cmp_lt_u32_e64 %5, %2, %3\n\t"
+          "v_cmp_lt_u32_e64 %4, %1, %2\n\tv_cmp_lt_u32_e64 %5, %3, %0\n\t"
+          "v_cmp_lt_u32_e64 %4, %0, %2\n\tv_cmp_lt_u32_e64 %5, %1, %3\n\t"
+          "v_cmp_lt_u32_e64 %4, %2, %1\n\tv_cmp_lt_u32_e64 %5, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=s"(m0), "=s"(m1));
+      s0 ^= (uint32_t)m0;
+      s1 ^= (uint32_t)(m1 >> 32);
+    } else if (KIND == 14) { // 8 v_cndmask_b32_e32 (mask in vcc)
+      asm volatile(
+          "s_mov_b64 vcc, %4\n\t"
+          "v_cndmask_b32_e32 %0, %0, %1, vcc\n\tv_cndmask_b32_e32 %1, %1, %2, vcc\n\t"
+          "v_cndmask_b32_e32 %2, %2, %3, vcc\n\tv_cndmask_b32_e32 %3, %3, %0, vcc\n\t"
+          "v_cndmask_b32_e32 %0, %0, %1, vcc\n\tv_cndmask_b32_e32 %1, %1, %2, vcc\n\t"
+          "v_cndmask_b32_e32 %2, %2, %3, vcc\n\tv_cndmask_b32_e32 %3, %3, %0, vcc\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d)
+          : "s"((uint64_t)s0 * 0x9E3779B97F4A7C15ull) : "vcc");
+    } else if (KIND == 15) { // 8 VOP2 with a 32-bit literal
+      asm volatile(
+          "v_and_b32_e32 %0, 0x7ff0f, %0\n\tv_add_u32_e32 %1, 0x12345, %1\n\t"
+          "v_xor_b32_e32 %2, 0x55aa55, %2\n\tv_or_b32_e32 %3, 0x8000, %3\n\t"
+          "v_and_b32_e32 %0, 0x7ff0f, %0\n\tv_add_u32_e32 %1, 0x12345, %1\n\t"
+          "v_xor_b32_e32 %2, 0x55aa55, %2\n\tv_or_b32_e32 %3, 0x8000, %3\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 16) { // 8 v_lshlrev_b32_e32 / v_lshrrev_b32_e32 / v_max_u32_e32 / v_sub_u32_e32
+      asm volatile(
+          "v_lshlrev_b32_e32 %0, 3, %0\n\tv_lshrrev_b32_e32 %1, 2, %1\n\t"
+          "v_max_u32_e32 %2, %2, %3\n\tv_sub_u32_e32 %3, %3, %0\n\t"
+          "v_lshlrev_b32_e32 %0, %1, %0\n\tv_lshrrev_b32_e32 %1, %2, %1\n\t"
+          "v_min_u32_e32 %2, %2, %0\n\tv_sub_u32_e32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 17) { // 8 v_cmp_*_e32 -> vcc (VOPC)
+      asm volatile(
+          "v_cmp_lt_u32_e32 vcc, %0, %1\n\tv_cmp_lt_u32_e32 vcc, %2, %3\n\t"
+          "v_cmp_lt_u32_e32 vcc, %1, %2\n\tv_cmp_lt_u32_e32 vcc, %3, %0\n\t"
+          "v_cmp_lt_u32_e32 vcc, %0, %2\n\tv_cmp_lt_u32_e32 vcc, %1, %3\n\t"
+          "v_cmp_lt_u32_e32 vcc, %2, %1\n\tv_cmp_lt_u32_e32 vcc, %3, %1\n\t"
+          "v_cndmask_b32_e32 %0, %0, %1, vcc\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : : "vcc");
+    } else if (KIND == 18) { // 8 v_mul_u32_u24_e32 (VOP2) / v_mad_u32_u24 (VOP3)
+      asm volatile(
+          "v_mul_u32_u24_e32 %0, %1, %0\n\tv_mul_u32_u24_e32 %1, %2, %1\n\t"
+          "v_mul_u32_u24_e32 %2, %3, %2\n\tv_mul_u32_u24_e32 %3, %0, %3\n\t"
+          "v_mul_u32_u24_e32 %0, %1, %0\n\tv_mul_u32_u24_e32 %1, %2, %1\n\t"
+          "v_mul_u32_u24_e32 %2, %3, %2\n\tv_mul_u32_u24_e32 %3, %0, %3\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 19) { // 8 VOP1: v_mov_b32 / v_not_b32 / v_ffbl_b32 / v_bfrev_b32
+      asm volatile(
+          "v_not_b32_e32 %0, %1\n\tv_ffbl_b32_e32 %1, %2\n\t"
+          "v_bfrev_b32_e32 %2, %3\n\tv_not_b32_e32 %3, %0\n\t"
+          "v_ffbl_b32_e32 %0, %1\n\tv_bfrev_b32_e32 %1, %2\n\t"
+          "v_not_b32_e32 %2, %3\n\tv_ffbl_b32_e32 %3, %0\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 20) { // 8 VOP2 with an SGPR operand
+      asm volatile(
+          "v_add_u32_e32 %0, %4, %0\n\tv_and_b32_e32 %1, %4, %1\n\t"
+          "v_xor_b32_e32 %2, %4, %2\n\tv_or_b32_e32 %3, %4, %3\n\t"
+          "v_add_u32_e32 %0, %4, %0\n\tv_and_b32_e32 %1, %4, %1\n\t"
+          "v_xor_b32_e32 %2, %4, %2\n\tv_or_b32_e32 %3, %4, %3\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "s"(s0));
+    } else if (KIND == 21) { // 8 v_add_u32_e64 (VOP2 op, VOP3 encoding)
+      asm volatile(
+          "v_add_u32_e64 %0, %0, %1\n\tv_add_u32_e64 %1, %1, %2\n\t"
+          "v_add_u32_e64 %2, %2, %3\n\tv_add_u32_e64 %3, %3, %0\n\t"
+          "v_xor_b32_e64 %0, %0, %2\n\tv_xor_b32_e64 %1, %1, %3\n\t"
+          "v_and_b32_e64 %2, %2, %0\n\tv_or_b32_e64 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 22) { // 8 v_readfirstlane / v_readlane (VALU -> SGPR)
+      uint32_t t0, t1;
+      asm volatile(
+          "v_readfirstlane_b32 %4, %0\n\tv_readlane_b32 %5, %1, 63\n\t"
+          "v_readfirstlane_b32 %4, %2\n\tv_readlane_b32 %5, %3, 63\n\t"
+          "v_readfirstlane_b32 %4, %1\n\tv_readlane_b32 %5, %0, 63\n\t"
+          "v_readfirstlane_b32 %4, %3\n\tv_readlane_b32 %5, %2, 63\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=s"(t0), "=s"(t1));
+      s0 ^= t0;
+      s1 ^= t1;
     } else {                 // 4 VALU + 4 SALU interleaved
       asm volatile(
           "v_add_u32 %0, %0, %1\n\ts_add_u32 %4, %4, %5\n\tv_add_u32 %1, %1, %2\n\t"
@@ -95,5 +237,24 @@ int main() {
     run<3>("v_mul_lo_u32", g, out, clk);
     run<4>("4 valu + 4 salu", g, out, clk);
   }
+  // the other VALU forms the compressor uses, at 8 waves per SIMD
+  run<5>("v_lshl/lshrrev_b64", grid, out, clk);
+  run<6>("v_alignbyte_b32", grid, out, clk);
+  run<7>("v_cndmask_b32_e64", grid, out, clk);
+  run<8>("v_add3 / v_lshl_add", grid, out, clk);
+  run<9>("v_mbcnt_lo/hi", grid, out, clk);
+  run<10>("v_perm_b32", grid, out, clk);
+  run<11>("v_mov_b32_dpp wave_shr", grid, out, clk);
+  run<12>("v_bfe / v_and_or", grid, out, clk);
+  run<13>("v_cmp_e64 -> sgpr", grid, out, clk);
+  run<14>("v_cndmask_b32_e32 vcc", grid, out, clk);
+  run<15>("VOP2 + literal", grid, out, clk);
+  run<16>("VOP2 shifts/max/sub", grid, out, clk);
+  run<17>("v_cmp_e32 -> vcc", grid, out, clk);
+  run<18>("v_mul_u32_u24_e32", grid, out, clk);
+  run<19>("VOP1 not/ffbl/bfrev", grid, out, clk);
+  run<20>("VOP2 + sgpr", grid, out, clk);
+  run<21>("v_add/xor_e64 (VOP3 enc)", grid, out, clk);
+  run<22>("v_readfirstlane/readlane", grid, out, clk);
   return 0;
 }
