@@ -1017,6 +1017,7 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   __shared__ alignas(16) uint8_t img[kEmitImg];
   __shared__ alignas(16) uint8_t stage[kStage];
   __shared__ uint32_t marks[kEW][64];                // per wave: literal-run starts
+  __shared__ uint2 pmask[9];                         // pmask[k]: the low k bytes of 8 set
   __shared__ uint32_t recst[kGH][kRecPre];           // each block's header + first records
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const size_t g = g_first + blockIdx.x / kGSplit;
@@ -1072,6 +1073,10 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   }
   if (hdr && g == 0 && h0 == 0 && tid == 0 && cap > 0) out[0] = (uint8_t)nb_total;
   if (tid < (h1 - h0) * kPerSlot) reinterpret_cast<uint4 *>(&recst[rhb][0])[rj] = rv;
+  if (tid < 9) {
+    const uint64_t m = tid == 8 ? ~0ull : (1ull << (8 * tid)) - 1ull;
+    pmask[tid] = make_uint2((uint32_t)m, (uint32_t)(m >> 32));
+  }
   // ---- stage: byte p of block h is stage[kStagePad + 300 (h - h0) + p] ----------
   {
     uint8_t *dst = stage + kStagePad;
@@ -1178,16 +1183,21 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
             if (gw < C) {
               const int t = 8 * ((int)(int16_t)(kw & 0xFFFFu) + gw);   // image word's first byte
               const int xs = t + ((int)kw >> 16);                      // its input bytes
-              const uint64_t *iw = reinterpret_cast<const uint64_t *>(stage + (xs & ~7));
-              const uint64_t lo = iw[0], hi = iw[1];
-              const uint32_t sh = 8u * (uint32_t)(xs & 7);
-              uint64_t v = (lo >> sh) | ((hi << 1) << (63u - sh));
-              // keep the run's bytes [lb, hb) of the word: shift the others out
-              const uint32_t l8 = 8u * (uint32_t)max((int)(kb & 0xFFFFu) - t, 0);
-              const uint32_t h8 = 64u - 8u * (uint32_t)min((int)(kb >> 16) - t, 8);
-              v = (v >> l8) << l8;
-              v = (v << h8) >> h8;
-              atomicOr(reinterpret_cast<unsigned long long *>(img + t), (unsigned long long)v);
+              // three aligned dwords and two v_alignbyte (64-bit shifts issue
+              // at ~5.6 cycles per wave-instruction, tools/valu_rate)
+              const uint32_t *iw = reinterpret_cast<const uint32_t *>(stage + (xs & ~3));
+              const uint32_t d0 = iw[0], d1 = iw[1], d2 = iw[2];
+              const uint32_t sh = (uint32_t)xs & 3u;
+              uint32_t v0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+              uint32_t v1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+              // keep the run's bytes [lb, hb) of the word: and with
+              // pmask[hb] ^ pmask[lb] (pmask[k] = the low k bytes set)
+              const int lb = max((int)(kb & 0xFFFFu) - t, 0), hb = min((int)(kb >> 16) - t, 8);
+              const uint2 ml = pmask[lb], mh = pmask[hb];
+              v0 &= ml.x ^ mh.x;
+              v1 &= ml.y ^ mh.y;
+              atomicOr(reinterpret_cast<unsigned long long *>(img + t),
+                       (unsigned long long)v1 << 32 | v0);
             }
           }
         }
