@@ -104,6 +104,24 @@ struct Bytes {
   }
 };
 
+// The same, unchecked, as a wave-uniform base and the lane's 32-bit offset
+// from it: every load is global_load with an SGPR base and a VGPR offset,
+// with no 64-bit address arithmetic on the walk's dependency chain (64-bit
+// VALU issues at ~5.6 cycles per wave-instruction on gfx950, a 32-bit add at
+// ~2.3: tools/valu_rate).
+struct BytesW {
+  const uint8_t *base;
+  uint32_t off;
+
+  __device__ __forceinline__ uint64_t ld8(int a) const {
+    return *reinterpret_cast<const u64u *>(base + (off + (uint32_t)a));
+  }
+  __device__ __forceinline__ V16 ld16(int a) const {
+    const uint32_t x = off + (uint32_t)a;
+    return {*reinterpret_cast<const u64u *>(base + x), *reinterpret_cast<const u64u *>(base + x + 8u)};
+  }
+};
+
 // The lane's 300-byte output slot in LDS.  Reads may run past the slot
 // (into a neighbour or the slack) and are masked by the caller; writes are
 // exact.
@@ -359,6 +377,9 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
 
   int q = 0;                                         // decoded bytes (0 = failed / absent)
   uint32_t pfv[kPfN] = {};
+  // the wave's base: its first block's first byte (a uniform load)
+  const size_t wbeg = 1 + boff[b0];
+  const uint8_t *const wbase = in + wbeg;
   if (lane < nl) {
     const bool last = b == nb - 1;
     const size_t beg = 1 + boff[b];
@@ -381,8 +402,10 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
       // unchecked loads only when that stays inside the stream, decided per
       // lane from its own offsets (caller-supplied offsets need not be
       // monotone; only the stream's last few blocks take the checked path)
-      if (beg + (size_t)kInMax + 64 <= in_len)
-        q = decode_block(Bytes<false>{in + beg, in_len - beg}, (int)(end - beg), last, o);
+      // (compressor offsets are monotone: the wave's blocks lie within
+      // 32 x kInMax bytes of its base; other offsets take the checked path)
+      if (beg + (size_t)kInMax + 64 <= in_len && beg >= wbeg && beg - wbeg < (1u << 30))
+        q = decode_block(BytesW{wbase, (uint32_t)(beg - wbeg)}, (int)(end - beg), last, o);
       else
         q = decode_block(Bytes<true>{in + beg, in_len - beg}, (int)(end - beg), last, o);
     }
