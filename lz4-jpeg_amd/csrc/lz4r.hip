@@ -735,6 +735,25 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
     wave_sync();
   }
   PROF_MARK(5);                       // walk
+#if LZ4R_VARIANT >= 40 && LZ4R_VARIANT <= 42
+  // tools build: probes of the binding resource -- 40: +16 conflict-free LDS
+  // reads, 41: +16 VOP3 VALU (v_perm), 42: +32 plain VALU (v_xor) per block
+  {
+    uint32_t acc = (uint32_t)lane;
+#if LZ4R_VARIANT == 40
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      acc ^= *reinterpret_cast<volatile uint32_t *>(&S.rec[(lane + 64 * (i & 3)) % kArr]);
+#elif LZ4R_VARIANT == 41
+#pragma unroll
+    for (int i = 0; i < 16; ++i) asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(acc) : "s"(0x05040100u));
+#else
+#pragma unroll
+    for (int i = 0; i < 32; ++i) asm volatile("v_xor_b32 %0, 0x9e3779b1, %0" : "+v"(acc));
+#endif
+    if (acc == 0x7FFFFFFFu) S.seq()[0] = acc;   // never on a real block; keeps the probe
+  }
+#endif
   // ---- sequence records: lane kk = sequence kk -----------------------------
   // A round is 64 consecutive sequences; the match sequences are a prefix
   // (cpos < n), followed by the literal-only tail when the last match ends
