@@ -101,3 +101,7 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all lib bin oracle tools sanitize clean
+
+# `make -s print-HIPFLAGS`: a variable's value (tests/test_isa.py builds with the product flags)
+print-%:
+	@echo $($*)

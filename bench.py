@@ -357,7 +357,7 @@ def run_lz4(ctx, n_total, scaling):
             _, got = comp.compress_device(d_in, n, d_out)
             return got
         comp.compress_async(d_in, n, d_out[1:], d_len, segment=True, final_shard=final_shard)
-        seg = int(d_len.item())
+        seg = comp.async_length(d_len)
         ldist.exchange_lengths(seg, dev)
         return seg
 
@@ -403,7 +403,7 @@ def run_lz4(ctx, n_total, scaling):
         _, flen = comp.compress_device(d_in, n, d_out)
     else:
         comp.compress_async(d_in, n, d_out[1:], d_len, segment=True, final_shard=final_shard)
-        flen = 1 + int(d_len.item())
+        flen = 1 + comp.async_length(d_len)
         d_out[0] = nb_local & 0xFF
     d_boff, _ = comp.block_offsets_device()
     d_dec = torch.empty(n + 300, dtype=torch.uint8, device=dev)
@@ -471,7 +471,7 @@ def run_lz4(ctx, n_total, scaling):
     gather_ms = gather_ok = None
     if world > 1:
         comp.compress_async(d_in, n, d_out[1:], d_len, segment=True, final_shard=final_shard)
-        seg = int(d_len.item())
+        seg = comp.async_length(d_len)
         lens, offs = ldist.exchange_lengths(seg, dev)
         torch.cuda.synchronize()
         ctx.barrier()
@@ -564,7 +564,7 @@ def run_cfg4_share(ctx, comp):
 
     def step():
         comp.compress_async(d_in, n, d_out, d_len, segment=True, final_shard=False)
-        return int(d_len.item())
+        return comp.async_length(d_len)
 
     comp.set_timing(True)                  # events made in the warm-up (two chunks here)
     for _ in range(max(1, args.warmup)):

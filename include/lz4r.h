@@ -47,7 +47,9 @@ extern "C" {
 #define LZ4R_ERR_CAPACITY (-3)    /* output buffer too small; *out_len = need */
 #define LZ4R_ERR_HIP (-4)         /* HIP runtime error */
 #define LZ4R_ERR_NOMEM (-5)       /* device allocation failed */
-#define LZ4R_ERR_CORRUPT (-6)     /* decoder: malformed stream */
+#define LZ4R_ERR_CORRUPT (-6)     /* decoder: malformed stream; compressor: corrupt LDS index */
+/* bit 63 of an async call's length word: the call met a corrupt LDS index */
+#define LZ4R_LEN_CORRUPT (1ull << 63)
 
 /* Inputs up to 2^40 bytes per call; the kernels run in chunks of 2^24 blocks
  * (5.03 GB), so device scratch is ~10.7 GB of block slots at most plus
@@ -73,7 +75,11 @@ int lz4r_compress_device(lz4r_ctx *ctx, const void *d_in, size_t n,
 
 /* Asynchronous form: enqueue only.  The compressed length (or the required
  * capacity, if larger than cap: nothing past cap is written) is stored as a
- * uint64 at d_out_len (device) when the stream reaches it. */
+ * uint64 at d_out_len (device) when the stream reaches it.  Bit 63 of that
+ * word (LZ4R_LEN_CORRUPT) is set, instead of an error return, when the call
+ * met a corrupt bucket head in lz4_tiles' LDS index (see lz4r_check): the
+ * caller gets the verdict in the same read-back as the length and must not
+ * use the stream then.  The length is the word without that bit. */
 int lz4r_compress_async(lz4r_ctx *ctx, const void *d_in, size_t n,
                         void *d_out, size_t cap, void *d_out_len,
                         void *stream);
@@ -180,11 +186,14 @@ int lz4r_decompress_stream(const uint8_t *in, size_t in_len, uint8_t *out, size_
 int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
                   size_t *out_len);
 
-/* Synchronise `stream` and report whether any compress call on ctx since the
- * last check met a corrupt bucket head in lz4_tiles' LDS index (a head that is
- * neither empty nor an earlier position of the block: never on a sound LDS;
- * the walk ends anyway, chains strictly decrease).  LZ4R_ERR_CORRUPT (and the
- * status is cleared) or LZ4R_OK.  lz4r_compress_device checks by itself. */
+/* Synchronise `stream` and report whether the last compress call on ctx met
+ * a corrupt bucket head in lz4_tiles' LDS index (a head that is neither empty
+ * nor an earlier position of the block: never on a sound LDS; the walk ends
+ * anyway, chains strictly decrease): LZ4R_ERR_CORRUPT or LZ4R_OK.  It reads
+ * LZ4R_LEN_CORRUPT of that call's length word; every call folds the kernel's
+ * status into its own length word and clears it, so an async caller that
+ * reads the length needs no separate check.  lz4r_compress_device checks by
+ * itself. */
 int lz4r_check(lz4r_ctx *ctx, void *stream);
 
 /* Measurement: when enabled, every compress call records HIP events on its

@@ -36,9 +36,11 @@
 //            has the largest distance (= smallest source, LZ4.c:307).  A
 //            running max over the lane's five and one wave max-scan give
 //            best() for all p.  M = len & 0xFF (the uint8_t return, LZ4.c:317).
-//     parse  nm(x) = first matchable position >= x; succ(c) = nm(c + M(c));
-//            the greedy parse (LZ4.c:516-583) is the walk c0 = nm(0),
-//            c_{k+1} = succ(c_k), one LDS read per sequence.
+//     parse  word[x] = the record word (dist | M << 9 | 4 (c + M) << 17) of
+//            c = the first matchable position >= x (a suffix pass over the
+//            positions); the greedy parse (LZ4.c:516-583) is the walk
+//            w_0 = word[0], w_{k+1} = word[c_k + M_k], one LDS read per
+//            sequence.
 //   records  sequence k on lane k: one packed wave scan of the bytes the block
 //            takes and of its size fields; record k = match start | M << 9 |
 //            dist << 17 (its literal run starts where sequence k - 1's match
@@ -156,9 +158,9 @@ struct TileLds {
   alignas(16) uint8_t buf[kBufBytes];
   union {
     uint32_t ent[kArr];   // per position: link | tag << 17 | preceding byte << 22
-    uint32_t nm[kArr];    // then: first matchable position >= x (dwords: no sub-dword LDS access)
+    uint32_t word[kArr];  // then: the first match at or after x, as its record word
   };
-  uint32_t rec[kArr];     // local(p) accumulator; then dist | M<<9 | succ<<17
+  uint32_t rec[kArr];     // local(p) accumulator: (p + len) << 9 | dist
   // chain walkers: the walker's byte offset 4 p (candidate phase)
   __device__ __forceinline__ uint32_t *q() { return reinterpret_cast<uint32_t *>(buf + kQOff); }
   // per sequence, its match start (slow walk only)
@@ -167,7 +169,11 @@ struct TileLds {
   __device__ __forceinline__ uint32_t *cand() { return reinterpret_cast<uint32_t *>(buf + kCandOff); }
 };
 
+constexpr int kWordOff = kBufBytes;             // byte offset of ent / word in TileLds
 constexpr int kRecOff = kBufBytes + 4 * kArr;   // byte offset of rec in TileLds
+// word[] past the last match: its field (the next read's byte offset) is
+// 4 * 319 > 4 n, the walk's exit, and stays inside the array
+constexpr uint32_t kWordEnd = (uint32_t)(4 * (kArr - 1)) << 17;
 static_assert(kHeadOff + 4 * kH <= kRecOff + 4 * 192, "u32 heads end before rec[192]");
 static_assert(kRecOff + 4 * kArr <= 4976, "LDS of one wave");
 
@@ -618,96 +624,64 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
     return 0;
   }
   // x = v - p << 9 = len << 9 | dist (len <= 0, i.e. x < 512 or negative,
-  // where no match covers p); the record's low 17 bits are dist | M << 9 with
-  // M = len & 0xFF (the uint8_t return, LZ4.c:317).  A match starts at p when
-  // len >= 4 and M != 0 (len 256 is a literal, LZ4.c:521); elsewhere the
-  // word's M and dist are 0 (the succ gather below then reads nm[p]: the
-  // lanes' stride-5 words, conflict-free; the lanes past the last match
-  // sequence read M = dist = 0 at rec[n]).
-  uint32_t mrec[5];
-  bool mt[5];                     // a match starts at p (M != 0)
-  int f[6];                       // f[r] = 4 x the first matchable position >= p0 + r
+  // where no match covers p); M = len & 0xFF (the uint8_t return, LZ4.c:317).
+  // A match starts at p when len >= 4 and M != 0 (len 256 is a literal,
+  // LZ4.c:521).
+  // The greedy parse (LZ4.c:516-583) at x -- 0, then the end of the previous
+  // match -- takes the first matchable position c = nm(x) >= x with its M and
+  // dist.  word[x] holds exactly that, as the match's own record word
+  //   dist | M << 9 | 4 (c + M) << 17
+  // whose top field is the byte offset of the next word the walk reads, or
+  // kWordEnd when no match starts at or after x.  So the walk reads one word
+  // per sequence and needs no successor table (no gathers, no second array).
+  uint32_t rw[5];                 // p's own word (where a match starts at p)
+  bool mt[5];                     // a match starts at p (len >= 4, M != 0)
   const uint32_t nP9 = 0u - ((uint32_t)p0 << 9);
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
-    // one v_add3; t = len << 9 | dist (M | dist) where len >= 4, else 0: a
-    // position with len 256 (M = 0) keeps its dist, which nothing reads
-    const uint32_t x = v[r] + nP9 + (0u - ((uint32_t)r << 9));
-    const uint32_t t = (int)x >= (4 << 9) ? x & 0x1FFFFu : 0u;
-    mt[r] = t >= 512u;
-    mrec[r] = t;
+    const uint32_t x = v[r] + nP9 + (0u - ((uint32_t)r << 9));   // one v_add3
+    const uint32_t M = (x >> 9) & 255u;                             // v_bfe
+    mt[r] = (int)x >= (4 << 9) && M != 0u;
+    rw[r] = ((M + (uint32_t)(p0 + r)) << 19) | (x & 0x1FFFFu);
   }
 
   PROF_MARK(3);                       // best scan
-  // ---- nm(x): first matchable position >= x, for x in [0, n] ---------------
-  // (as byte offsets 4 x: the serial walk then addresses the record words
-  // without a scalar shift per sequence)
+  // ---- word[x] for x in [0, n]: a suffix "next match" over the positions --
+  uint32_t w0;                    // word[0]: the first sequence's match
   {
-    int loc = 1 << 20;            // the lane's own first matchable position
+    uint32_t loc = kWordEnd;      // the lane's own first match word
 #pragma unroll
-    for (int r = 4; r >= 0; --r) loc = mt[r] ? 4 * (p0 + r) : loc;
-    const uint64_t has = ballot(loc < (1 << 20));
+    for (int r = 4; r >= 0; --r) loc = mt[r] ? rw[r] : loc;
+    const uint64_t has = ballot(loc != kWordEnd);
     const uint64_t up = has & ~((2ull << lane) - 1ull);  // lanes above this one
     const int src = up ? ctz64(up) : lane;
-    const int nx = __builtin_amdgcn_ds_bpermute(src << 2, loc);   // src in 0..63
-    f[5] = up ? nx : 4 * n;
+    const uint32_t nx = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)loc);
+    uint32_t w = up ? nx : kWordEnd;
+    uint32_t wr[5];
 #pragma unroll
-    for (int r = 4; r >= 0; --r) f[r] = mt[r] ? 4 * (p0 + r) : f[r + 1];
+    for (int r = 4; r >= 0; --r) wr[r] = w = mt[r] ? rw[r] : w;
 #pragma unroll
     for (int r = 0; r < 5; ++r)
-      S.nm[p0 + r] = f[r];               // past n: unused
+      S.word[p0 + r] = wr[r];            // past n: kWordEnd (no match starts there)
+    w0 = (uint32_t)__builtin_amdgcn_readlane((int)wr[0], 0);
   }
-  wave_sync();
-  // succ(p) = nm(p + M(p)) for the match starts, kept in the record word:
-  // rec[p] = dist | M << 9 | 4 succ << 17 (branch-free: the words of
-  // positions that start no match are written too, with M = dist = 0)
-  {
-    const uint32_t p4 = 4u * (uint32_t)p0;
-    uint32_t sj[5];
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      // nm[q + M], q = p0 + r (q + M <= n: matches end in the block); the
-      // byte address by v_bfe + v_lshl_add (the compiler's shift-and-mask
-      // form takes three); the five gathers go out before any store
-      uint32_t a;
-      asm("v_bfe_u32 %0, %1, 9, 8\n\tv_lshl_add_u32 %0, %0, 2, %2"
-          : "=&v"(a) : "v"(mrec[r]), "v"(p4));
-      sj[r] = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(S.nm) + a +
-                                                  4 * r);
-    }
-#pragma unroll
-    for (int r = 0; r < 5; ++r) S.rec[p0 + r] = mrec[r] | (sj[r] << 17);
-  }
-  const int F0 = __builtin_amdgcn_readlane(f[0], 0);    // nm(0)
   wave_sync();
 
-  PROF_MARK(4);                       // nm + succ
-  // ---- greedy parse = walk over match starts (LZ4.c:516-583) ---------------
-  // The walk is the serial part of the block: from c0 = nm(0), c_{k+1} =
-  // succ(c_k), one LDS read per sequence; sequence k's match start is kept
-  // in lane k of a register (v_writelane).  (A jump table of succ, succ^2,
-  // succ^3 took three sequences per read but cost two position-parallel
-  // gathers; with 8 waves per SIMD the walk's latency hides behind them.)
-  // (c4 = 4 c, the record word's byte offset)
-  const uint8_t *const recb = reinterpret_cast<const uint8_t *>(S.rec);
-  auto succ4 = [&](int c4) {
-    return (int)(__builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t *>(recb + c4)) >>
-                 17);
-  };
-  const int n4 = 4 * n;
-  int c4 = F0, it = 0;
-  // lane k of seqv: the record word whose successor field (bits 17..) is 4 c_k
-  // (for k = 0 a made-up word, F0 << 17).  Per sequence: the word goes to lane
-  // it (m0, which is also the counter: lane select = it mod 64; past 64
-  // sequences lanes are overwritten and the walk is redone below), the next
-  // word is read at the successor's byte offset, and the loop goes on while
-  // word < 4 n << 17 -- the same test as 4 c < 4 n, with no shift.  Two SALU
-  // and three VALU per sequence (a C++ loop took four SALU: m0 set from a
-  // counter, the counter, the shift, the compare).
+  PROF_MARK(4);                       // word
+  // ---- greedy parse = walk over the match words (LZ4.c:516-583) -------------
+  // The walk is the serial part of the block: w_0 = word[0], w_{k+1} =
+  // word[c_k + M_k], one LDS read per sequence; sequence k's word is kept in
+  // lane k of a register (v_writelane).  The loop is one asm block: m0 is both
+  // the lane select and the sequence counter, the next address is the loaded
+  // word shifted in a VGPR, and the loop goes on while the word is a match,
+  // i.e. its field 4 (c + M) <= 4 n (kWordEnd's is 4 * 319 > 4 n): three VALU
+  // and two SALU per sequence.
+  const uint32_t lim = (uint32_t)(4 * n + 1) << 17;
+  int it = 0;
   uint32_t seqv = 0;
-  if (c4 < n4) {
-    static_assert(kRecOff < 65536, "ds_read offset field");
-    uint32_t w = (uint32_t)F0 << 17, va = (uint32_t)F0, vt;
+  if (w0 < lim) {
+    static_assert(kWordOff < 65536, "ds_read offset field");
+    uint32_t w = w0, va = w0 >> 17, vt;
     asm volatile(
         "s_mov_b32 m0, 0\n"
         "1:\n\t"
@@ -721,15 +695,18 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
         "s_cbranch_scc1 1b\n\t"
         "s_mov_b32 %4, m0"
         : "+v"(seqv), "+s"(w), "+v"(va), "=&v"(vt), "=s"(it)
-        : "s"((uint32_t)n4 << 17), "i"(kRecOff)
+        : "s"(lim), "i"(kWordOff)
         : "scc", "memory");
   }
   // Past 64 sequences (only with truncated matches) the walk is redone into S.seq.
   const bool slow = it > 64;
   int Sv_slow = 0;
   if (slow) {
-    for (c4 = F0; c4 < n4; c4 = succ4(c4)) {
-      if (lane == 0) S.seq()[Sv_slow] = (uint32_t)c4 >> 2;
+    const uint8_t *const wb = reinterpret_cast<const uint8_t *>(S.word);
+    for (uint32_t w = w0; w < lim;
+         w = (uint32_t)__builtin_amdgcn_readfirstlane(
+             (int)*reinterpret_cast<const uint32_t *>(wb + (w >> 17)))) {
+      if (lane == 0) S.seq()[Sv_slow] = w;
       ++Sv_slow;
     }
     wave_sync();
@@ -767,14 +744,15 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
   int ocar = 3;                      // block header: u8 nseq, u16 size
   int szsum = 0;
   int end_prev = 0;                  // end of the previous round's last match
-  // one round: sequence kk = s0 + lane starts its match at cq (n past the
-  // matches); returns false once the round holds the last sequence
-  auto round = [&](int kk, uint32_t cq) {
+  // one round: sequence kk = s0 + lane has the match word wv (n << 19 -- no
+  // match, M = dist = 0, ending at n -- past the matches); returns false once
+  // the round holds the last sequence
+  auto round = [&](int kk, uint32_t wv) {
+    const int M = (int)((wv >> 9) & 255u);
+    const int end = (int)(wv >> 19);
+    const uint32_t cq = (uint32_t)(end - M);                       // the match start
     const bool ism = (int)cq < n;                                  // ends with a match
     const int nm_r = __popcll(ballot(ism));                        // a prefix of the round
-    const uint32_t rv = S.rec[cq];        // cq <= n; M = D = 0 at rec[n]: past the matches
-    const int M = (int)((rv >> 9) & 255u);
-    const int end = (int)cq + M;
     const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
     const int pend = lane == 0 ? end_prev : (int)upv;             // literal run start
     end_prev = (int)lane63((uint32_t)end);
@@ -792,7 +770,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
     ws += (uint32_t)(M - 1) < 3u ? 0x10000u : 0u;
     const uint32_t tot = lane63(wave_incl_add(sel_mask(am, ws, 0u)));
     if (sel_mask(am, 1u, 0u))
-      recs[1 + kk] = cq | (rv & 0x1FE00u) | ((rv & 511u) << 17);   // start | M | dist
+      recs[1 + kk] = cq | (wv & 0x1FE00u) | ((wv & 511u) << 17);   // start | M | dist
     ocar += (int)(tot & 0xFFFFu);
     szsum += (int)(tot >> 16);
     nseq += (int)__popcll(am);
@@ -801,11 +779,12 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
   if (LZ4R_VARIANT != 11) {
     // round 0 from the walk's register; more than 64 sequences (the walk's
     // register wrapped) come from the redone walk in S.seq
-    const uint32_t c0 = slow ? S.seq()[lane] : (lane < it ? seqv >> 19 : (uint32_t)n);
+    const uint32_t wtail = (uint32_t)n << 19;
+    const uint32_t c0 = slow ? S.seq()[lane] : (lane < it ? seqv : wtail);
     if (round(lane, c0)) {             // 64 match sequences: the tail or more follow
       for (int s0 = 64;; s0 += 64) {
         const int kk = s0 + lane;
-        if (!round(kk, slow && kk < Sv_slow ? S.seq()[kk] : (uint32_t)n)) break;
+        if (!round(kk, slow && kk < Sv_slow ? S.seq()[kk] : wtail)) break;
       }
     }
   }
@@ -960,10 +939,15 @@ __global__ __launch_bounds__(256) void lz4_scan_reduce(const uint32_t *__restric
 
 // one workgroup: exclusive scan of the partials in place, as absolute stream
 // offsets.  The scan starts at `hdr` (first != 0) or at *len (a continuation)
-// and leaves its end in *len.
+// and leaves its end in *len.  The call's last scan (last != 0) also folds
+// lz4_tiles' corrupt-index status word into bit 63 of *len (kLenCorrupt) and
+// clears the word: every async caller gets the verdict in the length it
+// reads anyway, and the next call starts clean.
+constexpr uint64_t kLenCorrupt = 1ull << 63;
 __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__ part,
                                                           size_t nparts, uint64_t hdr,
-                                                          int first,
+                                                          int first, int last,
+                                                          uint32_t *__restrict__ status,
                                                           uint64_t *__restrict__ len) {
   __shared__ uint64_t ws[16];
   __shared__ uint64_t carry;
@@ -987,7 +971,11 @@ __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__
     if (threadIdx.x == 1023) carry = pre + x;
     __syncthreads();
   }
-  if (threadIdx.x == 0) *len = carry;
+  if (threadIdx.x == 0) {
+    uint64_t v = carry;
+    if (last && atomicExch(status, 0u) != 0u) v |= kLenCorrupt;
+    *len = v;
+  }
 }
 
 
@@ -1279,6 +1267,7 @@ struct lz4r_ctx {
   uint64_t *len = nullptr;     // default device length slot, then the status word
   uint32_t *status = nullptr;  // (len + 1) nonzero once a block saw a corrupt bucket head
   size_t last_nb = 0;
+  uint64_t *last_len = nullptr;  // the last call's length slot (its bit 63: corrupt index)
   // timing: the call's start/end, and lz4_tiles' start/end in every chunk
   hipEvent_t ev_a = nullptr, ev_c = nullptr;
   std::vector<hipEvent_t> ev_tiles;   // 2 per chunk
@@ -1382,7 +1371,8 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
     hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)np), dim3(256), 0, s, c->tsz, b1, p0,
                        c->gsum, c->part);
     hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part + p0, np,
-                       (uint64_t)hdr, k == 0 ? 1 : 0, static_cast<uint64_t *>(d_len));
+                       (uint64_t)hdr, k == 0 ? 1 : 0, k + 1 == nchunks ? 1 : 0, c->status,
+                       static_cast<uint64_t *>(d_len));
     const size_t g0 = b0 / kGT, ng = (nbc + kGT - 1) / kGT;
     hipLaunchKernelGGL(lz4_emit, dim3((unsigned)(ng * kGSplit)), dim3(64 * kEW), 0, s, in, c->slots,
                        b0, c->tsz, b1, g0, c->gsum, c->part, static_cast<uint8_t *>(d_out),
@@ -1391,6 +1381,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   }
   if (timed) (void)hipEventRecord(c->ev_c, s);
   c->last_nb = nb;
+  c->last_len = static_cast<uint64_t *>(d_len);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess && getenv("LZ4R_DEBUG"))
     fprintf(stderr, "lz4r: %s\n", hipGetErrorString(e));
@@ -1458,6 +1449,7 @@ int lz4r_compress_segment_async(lz4r_ctx *c, const void *d_in, size_t n, void *d
   if (!final_shard && n % kBlk != 0) return LZ4R_ERR_ARG;
   if (n == 0) {                      // an empty shard (more ranks than blocks)
     c->last_nb = 0;
+    c->last_len = nullptr;
     c->timed_call = false;
     return hipMemsetAsync(d_len, 0, sizeof(uint64_t), static_cast<hipStream_t>(stream)) ==
                    hipSuccess
@@ -1472,20 +1464,17 @@ int lz4r_compress_device(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, s
   if (!c || !out_len) return LZ4R_ERR_ARG;
   int rc = run(c, d_in, n, d_out, cap, c->len, 1, stream);
   if (rc != LZ4R_OK) return rc;
-  uint64_t got[2] = {0, 0};            // the length and the status word: one read-back
+  uint64_t got = 0;                    // the length, with the corrupt flag: one read-back
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipError_t e = hipMemcpyAsync(got, c->len, sizeof(got), hipMemcpyDeviceToHost, s);
+  hipError_t e = hipMemcpyAsync(&got, c->len, sizeof(got), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     if (getenv("LZ4R_DEBUG")) fprintf(stderr, "lz4r: %s\n", hipGetErrorString(e));
     return LZ4R_ERR_HIP;
   }
-  *out_len = (size_t)got[0];
-  if ((uint32_t)got[1] != 0) {           // a corrupt bucket head: clear it, report it
-    (void)hipMemset(c->status, 0, sizeof(uint32_t));
-    return LZ4R_ERR_CORRUPT;
-  }
-  return got[0] > cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
+  *out_len = (size_t)(got & ~kLenCorrupt);
+  if (got & kLenCorrupt) return LZ4R_ERR_CORRUPT;   // a corrupt bucket head
+  return *out_len > cap ? LZ4R_ERR_CAPACITY : LZ4R_OK;
 }
 
 int lz4r_block_matches_device(const void *d_in, size_t n, void *d_matches, void *stream) {
@@ -1575,14 +1564,13 @@ int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t 
 
 int lz4r_check(lz4r_ctx *c, void *stream) {
   if (!c) return LZ4R_ERR_ARG;
-  uint32_t st = 0;
+  if (!c->last_len) return LZ4R_OK;      // no launch yet (or an empty segment)
+  uint64_t v = 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipMemcpyAsync(&st, c->status, sizeof(st), hipMemcpyDeviceToHost, s) != hipSuccess ||
+  if (hipMemcpyAsync(&v, c->last_len, sizeof(v), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return LZ4R_ERR_HIP;
-  if (st == 0) return LZ4R_OK;
-  (void)hipMemset(c->status, 0, sizeof(uint32_t));
-  return LZ4R_ERR_CORRUPT;
+  return (v & kLenCorrupt) ? LZ4R_ERR_CORRUPT : LZ4R_OK;
 }
 
 int lz4r_set_timing(lz4r_ctx *c, int enable) {

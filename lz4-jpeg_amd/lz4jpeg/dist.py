@@ -45,6 +45,13 @@ def exchange_lengths(seg_len, device, group=None):
     allv = torch.empty(world, dtype=torch.int64, device=device)
     dist.all_gather_into_tensor(allv, mine, group=group)
     lens = [int(x) for x in allv.cpu().tolist()]
+    if any(L < 0 for L in lens):
+        # a rank's HIP compressor flagged a corrupt LDS index (bit 63 of its
+        # length): every rank raises, none gathers a wrong stream
+        from .lz4 import Lz4Error
+        from ._lib import LZ4R_ERR_CORRUPT
+        bad = [r for r, L in enumerate(lens) if L < 0]
+        raise Lz4Error(LZ4R_ERR_CORRUPT, f"exchange_lengths: corrupt segment on rank(s) {bad}")
     offs, acc = [], 0
     for L in lens:
         offs.append(acc)
@@ -107,5 +114,7 @@ def hip_segment_compressor(compressor, final_shard, stream=None):
                                   final_shard=final_shard)
         if stream is not None:
             stream.synchronize()      # .item() below waits only for torch's current stream
-        return out, int(d_len.item())
+        # raises on a corrupt LDS index (bit 63 of the length): the segment
+        # never reaches the gather
+        return out, compressor.async_length(d_len)
     return run

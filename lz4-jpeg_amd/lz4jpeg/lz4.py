@@ -84,7 +84,9 @@ class Compressor:
 
     def compress_async(self, d_in, n, d_out, d_len, stream=None, segment=False,
                        final_shard=None):
-        """Enqueue only; the uint64 length lands in d_len (1-element int64 tensor).
+        """Enqueue only; the uint64 length lands in d_len (1-element int64 tensor),
+        with bit 63 set if the call met a corrupt LDS index: read it with
+        async_length(d_len), which raises then.
         segment=True: whole blocks without the frame header (one shard);
         final_shard must then be given: only the globally last shard may end
         in a short block, a non-final shard (final_shard=False) must be a
@@ -102,6 +104,18 @@ class Compressor:
             rc = L.lz4r_compress_async(*args, _stream_handle(stream))
         if rc != 0:
             _raise(rc, "lz4r_compress_segment_async" if segment else "lz4r_compress_async")
+
+    @staticmethod
+    def async_length(d_len):
+        """The length an async call stored in the int64 tensor d_len (reads it
+        back: waits for torch's current stream).  Raises Lz4Error(-6) when the
+        call flagged a corrupt LDS index (LZ4R_LEN_CORRUPT, bit 63: the int64
+        is negative) -- the stream must not be used then."""
+        v = int(d_len.item())
+        if v < 0:
+            raise Lz4Error(_lib.LZ4R_ERR_CORRUPT,
+                           "lz4r_compress_*_async: corrupt LDS index (LZ4R_LEN_CORRUPT)")
+        return v
 
     def block_offsets(self, count, stream=None):
         """numpy uint64 array: the last call's first `count` per-block output
@@ -124,8 +138,9 @@ class Compressor:
         return ptr.value, cnt.value
 
     def check(self, stream=None):
-        """lz4r_check: synchronise and raise Lz4Error(-6) if a call since the
-        last check met a corrupt bucket head (compress_device checks itself)."""
+        """lz4r_check: synchronise and raise Lz4Error(-6) if the last call met
+        a corrupt bucket head (compress_device and async_length check by
+        themselves)."""
         rc = _lib.lib().lz4r_check(self._h, _stream_handle(stream))
         if rc != 0:
             _raise(rc, "lz4r_check")
