@@ -314,6 +314,25 @@ __device__ __forceinline__ int lcp_keys(const uint32_t *kj, const uint32_t *kp, 
   return l < limit ? l : limit;
 }
 
+// The same from global memory (kFull blocks, whose bytes are not staged in
+// LDS: only a drain in the middle of the walk, when a pass could overflow the
+// candidate list, uses it): 16 bytes per operand and step as one unaligned
+// global_load_dwordx4 (L1/L2-resident: the block was just read).  Reads reach
+// at most 15 bytes past the block end, into the next block.
+__device__ __forceinline__ int lcp_global(const uint8_t *a, const uint8_t *b, int limit) {
+  int l = 0;
+  for (;;) {
+    uint4 A, B;
+    __builtin_memcpy(&A, a + l, 16);
+    __builtin_memcpy(&B, b + l, 16);
+    const uint32_t m = min(min(ffbl(A.x ^ B.x), ffbl(A.y ^ B.y) | 32u),
+                           min(ffbl(A.z ^ B.z) | 64u, ffbl(A.w ^ B.w) | 96u));
+    l += (int)min(m >> 3, 16u);
+    if (m != 0xFFFFFFFFu || l >= limit) break;
+  }
+  return l < limit ? l : limit;
+}
+
 // DPP helpers (gfx9 row_shr / row_bcast; identity 0 for lanes without a source)
 template <int CTRL, int ROW, int BANK>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -395,12 +414,17 @@ __device__ __forceinline__ void wave_sync() {
 // kMatchesOnly: stop after the best-match scan and store every position's
 // find_longest_match result to mout instead (lz4r_block_matches_device).
 template <bool kMatchesOnly, bool kFull>
-__device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__restrict__ mout,
+__device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t *__restrict__ gsrc,
+                                            uint32_t *__restrict__ mout,
                                             uint32_t *__restrict__ recs,
                                             uint32_t *__restrict__ status) {
-  // kFull: a whole 300-byte block (every block but possibly the last): n is
-  // a constant and only round 4's lanes 41..63 hold positions past the last
-  // 4-gram start
+  // kFull: a whole 300-byte block of a 4-byte aligned input that is not the
+  // launch's last (every block but one): n is a constant, only round 4's
+  // lanes 41..63 hold positions past the last 4-gram start, and the block is
+  // NOT staged in LDS -- each lane loads the two dwords its 4-grams need
+  // straight from gsrc (L1/L2: the 24 bytes past the block end that row 4
+  // reads belong to the next block); otherwise the block is staged at
+  // S.buf[kInOff] by the caller.
   const int n = kFull ? kBlk : n_arg;
   const int lane = threadIdx.x;
   constexpr int base = kInOff;
@@ -429,14 +453,17 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
   {
     // bytes p .. p + 3 from two aligned dwords: sh = p & 3 = lane & 3
     const uint32_t sh = (uint32_t)lane & 3u;
-    const uint32_t *bw = reinterpret_cast<const uint32_t *>(S.buf) + (kInOff >> 2) + (lane >> 2);
+    const uint32_t *bw = kFull ? reinterpret_cast<const uint32_t *>(gsrc) + (lane >> 2)
+                               : reinterpret_cast<const uint32_t *>(S.buf) + (kInOff >> 2) +
+                                     (lane >> 2);
     uint32_t pt[5], adr[5], set[5];
     // inactive positions (p >= nk) exchange with a dword of rec[192 + lane]
     // (past the heads, zeroed after the exchanges; distinct per lane)
     const uint32_t dummy = (uint32_t)(kRecOff + 4 * (192 + lane) - kHeadOff);
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-      const uint32_t w1 = bw[16 * r], w2 = bw[16 * r + 1];          // one ds_read2_b32
+      // one global_load_dwordx2 (kFull) or ds_read2_b32
+      const uint32_t w1 = bw[16 * r], w2 = bw[16 * r + 1];
       key[r] = __builtin_amdgcn_alignbyte(w2, w1, sh);
       // blk[p - 1] = byte 0 of key(p - 1): the lane below's key (DPP
       // wave_shr:1), for lane 0 lane 63's key of the round before (round 0's
@@ -525,7 +552,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, uint32_t *__r
         const uint32_t pr = S.cand()[i];
         const int p = (int)(pr & 0xFFFFu) >> 2, j = (int)(pr >> 18);   // j < p: chains decrease
         const int l = kKeys ? lcp_keys(S.q() + j, S.q() + p, n - p)
-                            : lcp(S.buf, base + j, base + p, n - p);
+                      : kFull ? lcp_global(gsrc + j, gsrc + p, n - p)
+                              : lcp(S.buf, base + j, base + p, n - p);
         // (end, dist) as the best scan wants it: for one p the larger end is
         // the longer match and the larger dist the smaller source
         if (LZ4R_VARIANT == 5) {          // ablation: the lcp without its result
@@ -809,29 +837,20 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   const int n = t == nb - 1 ? (int)last_n : kBlk;
   const uint8_t *src = in + (size_t)t * kBlk;
 
-  // ---- stage the block: 75 dwords, both loads in flight; 16-B zero pad ------
-  {
-    uint32_t *dst = reinterpret_cast<uint32_t *>(S.buf + kInOff);
-    if (kAligned && n == kBlk) {
-      // branch-free: the second load's address is clamped to the block's
-      // last dword, lanes 11.. store zeros -- the 48-B pad past the block
-      // and, for lanes 23.., dwords under the bucket heads, which are emptied
-      // after this
-      const uint32_t *q = reinterpret_cast<const uint32_t *>(src);
-      const uint32_t v0 = q[lane];
-      const uint32_t v1 = q[64 + min(lane, 10)];
-      dst[lane] = v0;
-      dst[64 + lane] = lane < 11 ? v1 : 0u;
-    } else {
-      for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
-      if (lane < 16) S.buf[kInOff + n + lane] = 0;
-    }
-  }
-  wave_sync();
-
   uint32_t *const recs = reinterpret_cast<uint32_t *>(slots + (size_t)t * kSlot);
-  const int W = n == kBlk ? encode_block<false, true>(S, n, nullptr, recs, status)
-                          : encode_block<false, false>(S, n, nullptr, recs, status);
+  int W;
+  if (kAligned && t + 1 < nb) {
+    // every block but the launch's last: no staging, the keys come straight
+    // from global memory (encode_block<kFull>)
+    W = encode_block<false, true>(S, kBlk, src, nullptr, recs, status);
+  } else {
+    // the last block (n <= 300: nothing may be read past the input) or an
+    // unaligned input: staged bytewise, 16-B zero pad
+    for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
+    if (lane < 16) S.buf[kInOff + n + lane] = 0;
+    wave_sync();
+    W = encode_block<false, false>(S, n, nullptr, nullptr, recs, status);
+  }
   if (lane == 0) {
     usz[t] = (uint32_t)W;
     bsizes[t] = (uint16_t)W;
@@ -851,7 +870,7 @@ __global__ __launch_bounds__(64) void lz4_matches(const uint8_t *__restrict__ in
   for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
   if (lane < 16) S.buf[kInOff + n + lane] = 0;
   wave_sync();
-  encode_block<true, false>(S, n, mout + (size_t)t * kBlk, nullptr, nullptr);
+  encode_block<true, false>(S, n, nullptr, mout + (size_t)t * kBlk, nullptr, nullptr);
 }
 
 // find_longest_match over a block of any length n (block_encode with a

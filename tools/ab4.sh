@@ -12,6 +12,10 @@ mkdir -p $O
 if [ -z "$AB_NOTEST" ]; then
   timeout -k 10 900 python -u -m pytest tests/test_gpu_lz4.py tests/test_gpu_compat.py tests/test_gpu_decode.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
   echo "tests: $(tail -1 $O/tests.log)"
+  for v in "$@"; do
+    LZ4JPEG_LIB=$PWD/tools/variants/liblz4_$v.so timeout -k 10 600 python -u -m pytest tests/test_gpu_lz4.py tests/test_gpu_compat.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests_$v.log 2>&1 || { echo "tests $v failed"; tail -30 $O/tests_$v.log; exit 1; }
+    echo "tests $v: $(tail -1 $O/tests_$v.log)"
+  done
 fi
 for pass in 1 2; do
   for v in prod "$@"; do
