@@ -60,6 +60,10 @@ def test_lz4_seq_committed_golden(tmp_path):
     assert run(exp, ["./LZ4_seq.exe"]).returncode == 0
     ref = open(os.path.join(golden_inputs.GOLDEN, "lz4_input.compressed.bin"), "rb").read()
     assert (tmp_path / "Output-Input/out/compressed.bin").read_bytes() == ref
+    # the hex dump (LZ4.c:75-107, written at :739) byte for byte against the
+    # reference's own committed Output-Input/out/compressed.txt
+    ref_txt = open(os.path.join(golden_inputs.GOLDEN, "lz4_input.compressed.txt"), "rb").read()
+    assert (tmp_path / "Output-Input/out/compressed.txt").read_bytes() == ref_txt
 
 
 def test_lz4_seq_too_small_exits_1(tmp_path):

@@ -33,6 +33,15 @@ def test_lz4_committed_compressed_bin_bytes(oracle):
     assert oracle.lz4_compress(data) == ref
 
 
+def test_lz4_committed_hex_dump(oracle):
+    """The reference's committed Output-Input/out/compressed.txt is the "%02X "
+    dump (LZ4.c:75-107) of its compressed.bin: pins the hex-dump format the
+    executables write, byte for byte, to a file the reference itself produced."""
+    data = open(os.path.join(golden_inputs.GOLDEN, "lz4_input.txt"), "rb").read()
+    ref = open(os.path.join(golden_inputs.GOLDEN, "lz4_input.compressed.txt"), "rb").read()
+    assert ref == "".join("%02X " % b for b in oracle.lz4_compress(data)).encode()
+
+
 def test_lz4_too_small(oracle):
     with pytest.raises(ValueError):
         oracle.lz4_compress(b"x" * 299)
