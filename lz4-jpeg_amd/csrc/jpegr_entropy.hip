@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/jpegr.h"
 
 namespace {
@@ -794,6 +796,47 @@ __global__ void entropy_init(ScratchHdr *hdr, uint32_t *status) {
   status[0] = 0;
 }
 
+// The decoder's luma and chroma kernels write disjoint outputs, and neither
+// fills the chip alone (a 4K image: 2,025 luma waves of 14.6 KB of LDS at 3
+// waves per SIMD, 4,050 chroma waves of 7 KB, each a single round of
+// one-lane-per-stream walks), so the chroma kernel runs on a side stream
+// beside the luma one (fork and join by events: the caller's stream waits for
+// both): 0.124 -> 0.115 ms per 4K image.  One side
+// stream per device, made on first use; the mutex serialises the enqueue of
+// concurrent callers (the launches stay asynchronous).
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+constexpr int kMaxDevices = 64;
+SideStream g_side[kMaxDevices];
+std::mutex g_side_mu;
+
+// Enqueue first(s) and second(side) so that they may run concurrently and
+// everything after them on s waits for both.
+template <typename F1, typename F2>
+int run_side_by_side(hipStream_t s, F1 first, F2 second) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return JPEGR_ERR_HIP;
+  std::lock_guard<std::mutex> lock(g_side_mu);
+  SideStream &sd = g_side[dev];
+  if (!sd.s) {
+    if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      return JPEGR_ERR_HIP;
+    }
+  }
+  if (hipEventRecord(sd.fork, s) != hipSuccess || hipStreamWaitEvent(sd.s, sd.fork, 0) != hipSuccess)
+    return JPEGR_ERR_HIP;
+  first(s);
+  second(sd.s);
+  if (hipEventRecord(sd.join, sd.s) != hipSuccess || hipStreamWaitEvent(s, sd.join, 0) != hipSuccess)
+    return JPEGR_ERR_HIP;
+  return JPEGR_OK;
+}
+
 }  // namespace
 
 extern "C" size_t jpegr_entropy_scratch_bytes(size_t ntiles) {
@@ -814,6 +857,9 @@ extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, vo
   auto *status = static_cast<uint32_t *>(d_status);
   hipLaunchKernelGGL(entropy_init, dim3(1), dim3(1), 0, s, hdr, status);
   const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
+  // (one stream: side by side, as the decoder runs, measured 0.140 -> 0.146 ms
+  // per 4K image -- the encoder's luma and chroma waves contend for the same
+  // LDS and issue slots, and the fork / join costs more than it overlaps)
   hipLaunchKernelGGL(entropy_encode_lane<true>, dim3(groups), dim3(kLanes), 0, s,
                      static_cast<const int16_t *>(d_coef), ntiles, static_cast<uint8_t *>(d_bits),
                      static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
@@ -840,13 +886,22 @@ extern "C" int jpegr_entropy_decode_device(const void *d_bits, const void *d_met
   if (hipMemsetAsync(static_cast<uint32_t *>(d_status) + 1, 0, sizeof(uint32_t), s) != hipSuccess)
     return JPEGR_ERR_HIP;
   const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
-  hipLaunchKernelGGL(entropy_decode_kernel<true>, dim3(groups), dim3(kLanes), 0, s,
-                     static_cast<const uint8_t *>(d_bits), static_cast<const uint32_t *>(d_meta),
-                     static_cast<const uint32_t *>(d_table), ntiles,
-                     static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
-  hipLaunchKernelGGL(entropy_decode_kernel<false>, dim3(groups * 2), dim3(kLanes), 0, s,
-                     static_cast<const uint8_t *>(d_bits), static_cast<const uint32_t *>(d_meta),
-                     static_cast<const uint32_t *>(d_table), ntiles,
-                     static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
+  const int rc = run_side_by_side(
+      s,
+      [&](hipStream_t q) {
+        hipLaunchKernelGGL(entropy_decode_kernel<true>, dim3(groups), dim3(kLanes), 0, q,
+                           static_cast<const uint8_t *>(d_bits),
+                           static_cast<const uint32_t *>(d_meta),
+                           static_cast<const uint32_t *>(d_table), ntiles,
+                           static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
+      },
+      [&](hipStream_t q) {
+        hipLaunchKernelGGL(entropy_decode_kernel<false>, dim3(groups * 2), dim3(kLanes), 0, q,
+                           static_cast<const uint8_t *>(d_bits),
+                           static_cast<const uint32_t *>(d_meta),
+                           static_cast<const uint32_t *>(d_table), ntiles,
+                           static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
+      });
+  if (rc != JPEGR_OK) return rc;
   return hipGetLastError() == hipSuccess ? JPEGR_OK : JPEGR_ERR_HIP;
 }

@@ -22,7 +22,7 @@ for pass in 1 2; do
     lib=""; [ $v = prod ] || lib=$PWD/tools/variants/liblz4_$v.so
     LZ4JPEG_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/p_${v}_$pass -o run -- python3 tools/lz4_one.py 1073741824 8 3 > $O/p_${v}_$pass.log 2>&1 || { tail -5 $O/p_${v}_$pass.log; exit 1; }
     echo "== $v pass $pass: $(tail -1 $O/p_${v}_$pass.log)"
-    python3 tools/prof_summary.py $O/p_${v}_$pass/run_results.db | grep -E 'lz4_(tiles|emit)' | head -2
+    python3 tools/prof_summary.py $O/p_${v}_$pass/run_results.db | grep -E 'lz4_(tiles|emit|pairs)' | head -3
   done
 done
 [ -n "$AB_NOPMC" ] || bash tools/lz4_ldsab.sh "$@"
