@@ -608,12 +608,16 @@ constexpr size_t kWorkBytesPerLane = 2 * kFullCap /*sym*/ + 2 * kFullCap /*hash*
 
 // Per stream up to 24 (luma) / 12 (chroma) codes, like the encoder's
 // working set (more: regenerated per symbol, decode_stream_slow): the
-// left-aligned codes in registers, each code's value | length in LDS
-// (14 / 7 KB per wave with the decoded ints, so a 4K image's 2,025 luma and
-// 4,050 chroma waves each run as one round of the chip's wave slots)
+// left-aligned codes in registers, each code's value and length in LDS as one
+// u16 (value in 11 bits, two's complement, | length << 11: every value of a
+// 4K image's streams fits; a stream whose values or lengths do not takes the
+// slow path), in a dword-column layout (two codes per dword of the lane's own
+// bank).  11.5 / 5.9 KB per wave with the decoded ints: a 4K image's 2,025
+// luma waves and 2,025 chroma waves (a lane decodes the tile's Cr, then its
+// Cb stream) are all resident at once, the two kernels side by side.
 template <int N, int Cap>
 struct DecLds {
-  uint32_t vl[Cap][kLanes];                // value | len << 16 (the codes are in registers)
+  uint32_t vl[Cap / 2][kLanes];            // codes 2i, 2i + 1: value | len << 11 (u16 each)
   // the lane's decoded ints; rows of N + 2 (an odd number of dwords), so the
   // lanes' stores at one index hit 64 different banks (rows of N: 32-way)
   alignas(16) int16_t out[kLanes][N + 2];
@@ -628,31 +632,36 @@ struct DecLds {
 // count of codes <= the window, minus one -- Cap independent compares
 // instead of a binary search whose every step waited on an LDS read.  Only
 // the matched entry's value | length is read from LDS (vl).
+// Returns 1 (decoded), 0 (malformed) or -1 (a value or length that the u16
+// entries cannot hold: the caller runs decode_stream_slow).
 template <int Cap, typename VlT>
-__device__ bool decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
-                              const uint32_t *__restrict__ table, VlT vl,
-                              int16_t *__restrict__ out, int n) {
+__device__ int decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
+                             const uint32_t *__restrict__ table, VlT vl,
+                             int16_t *__restrict__ out, int n) {
   const int nbits = (int)(m & 0xFFFF), R = (int)((m >> 16) & 255), U = (int)(m >> 24);
-  if (U == 0 || U > Cap || R == 0 || R > 2 * n) return false;
+  if (U == 0 || U > Cap || R == 0 || R > 2 * n) return 0;
   // codes from the lengths, left to right (DFS order)
   uint32_t lc[Cap];
   uint32_t code = 0;
   int plen = 0;
-  bool bad = false;
+  bool bad = false, wide = false;
 #pragma unroll
   for (int k = 0; k < Cap; ++k) {
     lc[k] = ~0u;
     if (k < U) {
       const uint32_t e = table[k];
       const int L = (int)((e >> 16) & 255);
+      const int v = (int16_t)(e & 0xFFFF);
       bad = bad || L > 32 || (U > 1 && L == 0);
+      wide = wide || L > 31 || v < -1024 || v > 1023;
       if (k) code = L >= plen ? (code + 1) << (L - plen) : (code + 1) >> (plen - L);
       plen = L;
       lc[k] = L ? code << (32 - L) : 0;
-      vl[k] = e;
+      vl[k] = (uint16_t)(((uint32_t)v & 0x7FFu) | ((uint32_t)L << 11));
     }
   }
-  if (bad) return false;
+  if (bad) return 0;
+  if (wide) return -1;
   int idx = 0, pending = -1;                        // pending: a count awaiting its value
   auto put = [&](int v) {
     if (pending < 0) {
@@ -664,8 +673,10 @@ __device__ bool decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
     if (idx + cnt > n) cnt = n - idx;
     for (int j = 0; j < cnt; ++j) out[idx++] = (int16_t)v;
   };
+  // an entry's value (11-bit two's complement) and length
+  auto val = [](uint32_t e) { return (int)((int32_t)(e << 21) >> 21); };
   if (U == 1) {
-    const int v = (int16_t)(vl[0] & 0xFFFF);
+    const int v = val(vl[0]);
     for (int j = 0; j < R; ++j) put(v);
   } else {
     // MSB-first bit buffer: acc holds nacc valid bits, left-aligned; words
@@ -698,18 +709,18 @@ __device__ bool decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
 #pragma unroll
       for (int k = 0; k < Cap; ++k) cnt += lc[k] <= win ? 1 : 0;
       const uint32_t e = vl[min(cnt, U) - 1];
-      const int L = (int)((e >> 16) & 255);
-      if (p + L > nbits || L == 0) return false;
-      put((int16_t)(e & 0xFFFF));
+      const int L = (int)(e >> 11);
+      if (p + L > nbits || L == 0) return 0;
+      put(val(e));
       p += L;
       acc <<= L;
       nacc -= L;
       ++got;
     }
-    if (got != R) return false;
+    if (got != R) return 0;
   }
   while (idx < n) out[idx++] = 0;
-  return true;
+  return 1;
 }
 
 // Streams with more codes than the LDS table holds (> 24 luma / 12 chroma:
@@ -755,7 +766,8 @@ __device__ bool decode_stream_slow(const uint8_t *__restrict__ bits, uint32_t m,
   return true;
 }
 
-// luma and chroma waves apart, as in the encoder (their output slots differ)
+// luma and chroma waves apart, as in the encoder (their output slots
+// differ); a chroma lane decodes its tile's Cr stream, then its Cb stream
 template <bool kLuma>
 __global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
     const uint8_t *__restrict__ bits, const uint32_t *__restrict__ meta,
@@ -764,31 +776,35 @@ __global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
   constexpr int Cap = kLuma ? kFastCap : kChromaCap;
   __shared__ DecLds<kLuma ? 64 : 32, Cap> S;
   const int lane = threadIdx.x;
-  const int c = kLuma ? 0 : 1 + (int)(blockIdx.x & 1);
-  const size_t tile = (size_t)(kLuma ? blockIdx.x : blockIdx.x >> 1) * kLanes + lane;
+  const size_t tile = (size_t)blockIdx.x * kLanes + lane;
   if (tile >= ntiles) return;
-  const uint32_t m = meta[tile * 3 + c];
-  const int U = (int)(m >> 24);
-  const uint8_t *b = bits + tile * kBitsPerTile + bits_off(c);
-  const uint32_t *t = table + tile * kTablePerTile + bits_off(c);
   // ints are produced one at a time: collect them in LDS, then 16-B stores
   // (2-byte stores to 64 scattered streams wrote ~6x the bytes)
   int16_t *o = S.out[lane];
-  const int n = stream_len(c);
-  // a foreign or corrupted meta word must not index past the stream's slot:
-  // its bits (bits_cap bits) and its table (2 n entries: RLE of n ints)
-  const bool sane = (int)(m & 0xFFFF) <= bits_cap(c) && U <= 2 * n;
-  const bool ok = sane && (U <= Cap
-                               ? decode_stream<Cap>(b, m, t, Col<uint32_t>{&S.vl[0][lane], kLanes},
-                                                    o, n)
-                               : decode_stream_slow(b, m, t, o, n));
-  if (!sane)
-    for (int j = 0; j < n; ++j) o[j] = 0;
-  if (!ok) atomicAdd(&status[1], 1u);
-  uint4 *dst = reinterpret_cast<uint4 *>(coef + tile * 128 + coef_off(c));
-  const uint32_t *src = reinterpret_cast<const uint32_t *>(o);    // 4-B aligned rows
-  for (int v = 0; v < n / 8; ++v)
-    dst[v] = make_uint4(src[4 * v], src[4 * v + 1], src[4 * v + 2], src[4 * v + 3]);
+  const LCol<uint16_t> vl{reinterpret_cast<uint8_t *>(&S.vl[0][lane])};
+#pragma unroll 1
+  for (int c = kLuma ? 0 : 1; c <= (kLuma ? 0 : 2); ++c) {
+    const uint32_t m = meta[tile * 3 + c];
+    const int U = (int)(m >> 24);
+    const uint8_t *b = bits + tile * kBitsPerTile + bits_off(c);
+    const uint32_t *t = table + tile * kTablePerTile + bits_off(c);
+    const int n = stream_len(c);
+    // a foreign or corrupted meta word must not index past the stream's
+    // slot: its bits (bits_cap bits) and its table (2 n entries: RLE of n ints)
+    const bool sane = (int)(m & 0xFFFF) <= bits_cap(c) && U <= 2 * n;
+    bool ok = false;
+    if (sane) {
+      const int r = U <= Cap ? decode_stream<Cap>(b, m, t, vl, o, n) : -1;
+      ok = r < 0 ? decode_stream_slow(b, m, t, o, n) : r != 0;
+    } else {
+      for (int j = 0; j < n; ++j) o[j] = 0;
+    }
+    if (!ok) atomicAdd(&status[1], 1u);
+    uint4 *dst = reinterpret_cast<uint4 *>(coef + tile * 128 + coef_off(c));
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(o);    // 4-B aligned rows
+    for (int v = 0; v < n / 8; ++v)
+      dst[v] = make_uint4(src[4 * v], src[4 * v + 1], src[4 * v + 2], src[4 * v + 3]);
+  }
 }
 
 __global__ void entropy_init(ScratchHdr *hdr, uint32_t *status) {
@@ -797,11 +813,10 @@ __global__ void entropy_init(ScratchHdr *hdr, uint32_t *status) {
 }
 
 // The decoder's luma and chroma kernels write disjoint outputs, and neither
-// fills the chip alone (a 4K image: 2,025 luma waves of 14.6 KB of LDS at 3
-// waves per SIMD, 4,050 chroma waves of 7 KB, each a single round of
-// one-lane-per-stream walks), so the chroma kernel runs on a side stream
-// beside the luma one (fork and join by events: the caller's stream waits for
-// both): 0.124 -> 0.115 ms per 4K image.  One side
+// fills the chip alone (a 4K image: 2,025 luma waves of 11.5 KB of LDS and
+// 2,025 chroma waves of 5.9 KB, each a single round of one-lane-per-stream
+// walks), so the chroma kernel runs on a side stream beside the luma one
+// (fork and join by events: the caller's stream waits for both).  One side
 // stream per device, made on first use; the mutex serialises the enqueue of
 // concurrent callers (the launches stay asynchronous).
 struct SideStream {
@@ -896,7 +911,7 @@ extern "C" int jpegr_entropy_decode_device(const void *d_bits, const void *d_met
                            static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
       },
       [&](hipStream_t q) {
-        hipLaunchKernelGGL(entropy_decode_kernel<false>, dim3(groups * 2), dim3(kLanes), 0, q,
+        hipLaunchKernelGGL(entropy_decode_kernel<false>, dim3(groups), dim3(kLanes), 0, q,
                            static_cast<const uint8_t *>(d_bits),
                            static_cast<const uint32_t *>(d_meta),
                            static_cast<const uint32_t *>(d_table), ntiles,
