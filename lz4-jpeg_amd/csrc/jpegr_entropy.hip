@@ -623,6 +623,64 @@ struct DecLds {
   alignas(16) int16_t out[kLanes][N + 2];
 };
 
+// The number of k < Cap with h[k] > w (31-bit values): the borrows of
+// w - h[k], taken by v_sub_co_u32 into SGPR pairs and summed by
+// v_addc_co_u32 in two chains, eight codes per asm block (each carry is read
+// at least eight instructions after its write: no hazard wait states; a
+// group of four pads with an s_nop).
+template <int Cap>
+__device__ __forceinline__ int count_above(uint32_t w, const uint32_t (&h)[Cap]) {
+  static_assert(Cap % 4 == 0, "groups of four");
+  uint32_t a = 0, b = 0;
+  if constexpr (Cap % 8 == 4) {
+    uint32_t t0, t1, t2, t3;
+    uint64_t c0, c1, c2, c3, d0, d1;
+    asm("v_sub_co_u32_e64 %[t0], %[c0], %[w], %[h0]\n\t"
+        "v_sub_co_u32_e64 %[t1], %[c1], %[w], %[h1]\n\t"
+        "v_sub_co_u32_e64 %[t2], %[c2], %[w], %[h2]\n\t"
+        "v_sub_co_u32_e64 %[t3], %[c3], %[w], %[h3]\n\t"
+        "s_nop 1\n\t"
+        "v_addc_co_u32_e64 %[a], %[d0], %[a], 0, %[c0]\n\t"
+        "v_addc_co_u32_e64 %[b], %[d1], %[b], 0, %[c1]\n\t"
+        "v_addc_co_u32_e64 %[a], %[d0], %[a], 0, %[c2]\n\t"
+        "v_addc_co_u32_e64 %[b], %[d1], %[b], 0, %[c3]"
+        : [a] "+v"(a), [b] "+v"(b), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [c0] "=&s"(c0), [c1] "=&s"(c1), [c2] "=&s"(c2), [c3] "=&s"(c3),
+          [d0] "=&s"(d0), [d1] "=&s"(d1)
+        : [w] "v"(w), [h0] "v"(h[Cap - 4]), [h1] "v"(h[Cap - 3]), [h2] "v"(h[Cap - 2]),
+          [h3] "v"(h[Cap - 1]));
+  }
+#pragma unroll
+  for (int g = 0; g + 8 <= Cap; g += 8) {
+    uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+    uint64_t c0, c1, c2, c3, c4, c5, c6, c7, d0, d1;
+    asm("v_sub_co_u32_e64 %[t0], %[c0], %[w], %[h0]\n\t"
+        "v_sub_co_u32_e64 %[t1], %[c1], %[w], %[h1]\n\t"
+        "v_sub_co_u32_e64 %[t2], %[c2], %[w], %[h2]\n\t"
+        "v_sub_co_u32_e64 %[t3], %[c3], %[w], %[h3]\n\t"
+        "v_sub_co_u32_e64 %[t4], %[c4], %[w], %[h4]\n\t"
+        "v_sub_co_u32_e64 %[t5], %[c5], %[w], %[h5]\n\t"
+        "v_sub_co_u32_e64 %[t6], %[c6], %[w], %[h6]\n\t"
+        "v_sub_co_u32_e64 %[t7], %[c7], %[w], %[h7]\n\t"
+        "v_addc_co_u32_e64 %[a], %[d0], %[a], 0, %[c0]\n\t"
+        "v_addc_co_u32_e64 %[b], %[d1], %[b], 0, %[c1]\n\t"
+        "v_addc_co_u32_e64 %[a], %[d0], %[a], 0, %[c2]\n\t"
+        "v_addc_co_u32_e64 %[b], %[d1], %[b], 0, %[c3]\n\t"
+        "v_addc_co_u32_e64 %[a], %[d0], %[a], 0, %[c4]\n\t"
+        "v_addc_co_u32_e64 %[b], %[d1], %[b], 0, %[c5]\n\t"
+        "v_addc_co_u32_e64 %[a], %[d0], %[a], 0, %[c6]\n\t"
+        "v_addc_co_u32_e64 %[b], %[d1], %[b], 0, %[c7]"
+        : [a] "+v"(a), [b] "+v"(b), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7),
+          [c0] "=&s"(c0), [c1] "=&s"(c1), [c2] "=&s"(c2), [c3] "=&s"(c3), [c4] "=&s"(c4),
+          [c5] "=&s"(c5), [c6] "=&s"(c6), [c7] "=&s"(c7), [d0] "=&s"(d0), [d1] "=&s"(d1)
+        : [w] "v"(w), [h0] "v"(h[g]), [h1] "v"(h[g + 1]), [h2] "v"(h[g + 2]),
+          [h3] "v"(h[g + 3]), [h4] "v"(h[g + 4]), [h5] "v"(h[g + 5]), [h6] "v"(h[g + 6]),
+          [h7] "v"(h[g + 7]));
+  }
+  return (int)(a + b);
+}
+
 // Decode one stream: bits + table -> RLE ints (decode_huffman) -> n ints
 // (inverse_RLE: counts clamped to n, zero fill).  With one code (empty bit
 // string) the reference decodes nothing and keeps its RLE ints: rle_len
@@ -687,8 +745,11 @@ __device__ int decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
     int qi = 0, ci = 1;
     uint64_t acc = 0;
     int nacc = 0, p = 0, got = 0;
+    uint32_t lh[Cap];
+#pragma unroll
+    for (int k = 0; k < Cap; ++k) lh[k] = lc[k] >> 1;
     while (p < nbits) {
-      while (nacc <= 32) {                            // refill 32 bits
+      if (nacc <= 32) {                               // refill 32 bits (codes <= 31)
         const uint32_t wd = qi == 0 ? q.x : qi == 1 ? q.y : qi == 2 ? q.z : q.w;
         acc |= (uint64_t)__builtin_bswap32(wd) << (32 - nacc);
         nacc += 32;
@@ -704,20 +765,27 @@ __device__ int decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
       if (nbits - p < 32) win &= ~0u << (32 - (nbits - p));
       // largest k with lc[k] <= win: the codes increase, so it is the count
       // of codes <= win, minus one (lc[0] = 0; the all-ones entries past U
-      // count only for an all-ones window, whose code is the last)
-      int cnt = 0;
-#pragma unroll
-      for (int k = 0; k < Cap; ++k) cnt += lc[k] <= win ? 1 : 0;
+      // count only for an all-ones window, whose code is the last).  Counted
+      // as Cap minus the borrows of win - lc[k] on 31 bits (a code of <= 31
+      // bits leaves bit 0 of its left-aligned form clear, so dropping it
+      // loses nothing), in two carry chains through SGPR pairs: the
+      // compare-and-add form serialised every code on VCC with two wait
+      // states each (decode 0.106 -> 0.099 ms with the branch-free
+      // malformed-code check and the single-step refill)
+      const int cnt = Cap - count_above<Cap>(win >> 1, lh);
       const uint32_t e = vl[min(cnt, U) - 1];
       const int L = (int)(e >> 11);
-      if (p + L > nbits || L == 0) return 0;
-      put(val(e));
-      p += L;
+      // a code past the end (or of length 0) ends the walk as malformed:
+      // flagged, no branch out of the loop per symbol
+      const bool badsym = p + L > nbits || L == 0;
+      bad = bad || badsym;
+      if (!badsym) put(val(e));
+      p = badsym ? nbits : p + L;
       acc <<= L;
       nacc -= L;
       ++got;
     }
-    if (got != R) return 0;
+    if (bad || got != R) return 0;
   }
   while (idx < n) out[idx++] = 0;
   return 1;
