@@ -39,13 +39,13 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TOPS = 39.3     # 78.6 TFLOPS fp64 vector spec counts FMA as 2
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # (tools/traffic.sh -> tools/traffic_summary.py, gfx950 FETCH correction applied)
-TRAFFIC_JSON = os.path.join(REPO, "profiles", "r03_traffic.json")
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r04_traffic.json")
 # per-launch instruction counts of lz4_tiles + measured SIMD issue rates
 # (tools/issue.sh -> tools/issue_summary.py)
-ISSUE_JSON = os.path.join(REPO, "profiles", "r03_issue.json")
+ISSUE_JSON = os.path.join(REPO, "profiles", "r04_issue.json")
 # clock each kernel holds under its own load (DVFS give-back), from a
 # GRBM_GUI_ACTIVE PMC pass (tools/clock_pmc.sh -> tools/clock_summary.py)
-CLOCK_JSON = os.path.join(REPO, "profiles", "r03_clock.json")
+CLOCK_JSON = os.path.join(REPO, "profiles", "r04_clock.json")
 SPEC_CLOCK_GHZ = 2.4
 
 CFG4_BYTES = 64 << 30          # configs[3]
@@ -59,8 +59,8 @@ def log(*a):
 
 def _profile_json(path):
     """This round's profile, else the latest earlier round's."""
-    for r in ("r03_", "r02_", "r01_"):
-        p = path.replace("r03_", r)
+    for r in ("r04_", "r03_", "r02_", "r01_"):
+        p = path.replace("r04_", r)
         if os.path.exists(p):
             return p
     return path
