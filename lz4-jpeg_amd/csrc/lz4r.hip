@@ -42,9 +42,10 @@
 //            w_0 = word[0], w_{k+1} = word[c_k + M_k], one LDS read per
 //            sequence.
 //   records  sequence k on lane k: one packed wave scan of the bytes the block
-//            takes and of its size fields; record k = match start | M << 9 |
-//            dist << 17 (its literal run starts where sequence k - 1's match
-//            ends) -> the block's slot, after a header dword (sum of the size
+//            takes and of its size fields; record k = the sequence's match
+//            word dist | M << 9 | (match start + M) << 19 (its literal run
+//            starts where sequence k - 1's match ends; the literal tail is
+//            n << 19) -> the block's slot, after a header dword (sum of the size
 //            fields | sequence count << 16); the block's byte count -> usz
 //            (u32, for the scan) and bsizes (u16).
 // lz4_scan_reduce / lz4_scan_partials: exclusive scan of the block sizes.
@@ -534,6 +535,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
   // Candidates go to a list in S.cand, drained by a balanced lcp pass with
   // LDS atomicMax into S.rec ((p + len) << 9 | (p - j): the longest, ties to
   // the smallest j).
+  uint32_t longm = 0;                    // this lane verified a candidate of >= 256 bytes
   if (search && LZ4R_VARIANT != 3) {
     constexpr int kTrash = kCand - 1;
     int ncand = 0;
@@ -560,6 +562,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
         } else if (l >= 4) {
           atomicMax(&S.rec[p], ((uint32_t)(p + l) << 9) | (uint32_t)(p - j));
         }
+        longm |= l >= 256 ? 1u : 0u;     // (a match the uint8_t return truncates)
       }
       wave_sync();
     };
@@ -661,21 +664,27 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
   // whose top field is the byte offset of the next word the walk reads, or
   // kWordEnd when no match starts at or after x.  So the walk reads one word
   // per sequence and needs no successor table (no gathers, no second array).
-  uint32_t rw[5];                 // p's own word (where a match starts at p)
-  bool mt[5];                     // a match starts at p (len >= 4, M != 0)
+  // (the word pass is instantiated for both cases below, so the match flags
+  // stay lane masks in SGPRs: merged across a branch they were packed into
+  // a VGPR and unpacked again, ~15 VALU)
   const uint32_t nP9 = 0u - ((uint32_t)p0 << 9);
+  auto word_pass = [&](auto fast) -> uint32_t {
+    uint32_t rw[5];               // p's own word (where a match starts at p)
+    bool mt[5];                   // a match starts at p (len >= 4, M != 0)
 #pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const uint32_t x = v[r] + nP9 + (0u - ((uint32_t)r << 9));   // one v_add3
-    const uint32_t M = (x >> 9) & 255u;                             // v_bfe
-    mt[r] = (int)x >= (4 << 9) && M != 0u;
-    rw[r] = ((M + (uint32_t)(p0 + r)) << 19) | (x & 0x1FFFFu);
-  }
-
-  PROF_MARK(3);                       // best scan
-  // ---- word[x] for x in [0, n]: a suffix "next match" over the positions --
-  uint32_t w0;                    // word[0]: the first sequence's match
-  {
+    for (int r = 0; r < 5; ++r) {
+      const uint32_t x = v[r] + nP9 + (0u - ((uint32_t)r << 9));   // one v_add3
+      if constexpr (decltype(fast)::value) {
+        mt[r] = (int)x >= (4 << 9);
+        rw[r] = ((v[r] << 10) & 0xFFF80000u) | (x & 0x7FFFFu);   // one v_bfi
+      } else {
+        const uint32_t M = __builtin_amdgcn_ubfe(x, 9, 8);
+        mt[r] = (int)x >= (4 << 9) && M != 0u;
+        rw[r] = ((M + (uint32_t)(p0 + r)) << 19) | (x & 0x1FFFFu);
+      }
+    }
+    PROF_MARK(3);                     // best scan
+    // ---- word[x] for x in [0, n]: a suffix "next match" over the positions
     uint32_t loc = kWordEnd;      // the lane's own first match word
 #pragma unroll
     for (int r = 4; r >= 0; --r) loc = mt[r] ? rw[r] : loc;
@@ -690,8 +699,16 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
 #pragma unroll
     for (int r = 0; r < 5; ++r)
       S.word[p0 + r] = wr[r];            // past n: kWordEnd (no match starts there)
-    w0 = (uint32_t)__builtin_amdgcn_readlane((int)wr[0], 0);
-  }
+    return (uint32_t)__builtin_amdgcn_readlane((int)wr[0], 0);   // word[0]
+  };
+  // No verified candidate reached 256 bytes, so no best(p) does (a scan term
+  // is a candidate shifted right, never longer): len < 256, M = len, every
+  // len >= 4 is a match, and the word's field c + M is the scan value's end:
+  // rw = (end << 19) | (len << 9 | dist), the shifted scan value over x by one
+  // v_bfi (x's bits 17..18 are len's bits 8..9: zero).  Otherwise the general
+  // form (M = len & 0xFF, len 256 no match).
+  const uint32_t w0 = ballot(longm != 0u) ? word_pass(std::false_type{})
+                                           : word_pass(std::true_type{});
   wave_sync();
 
   PROF_MARK(4);                       // word
@@ -762,10 +779,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
   // A round is 64 consecutive sequences; the match sequences are a prefix
   // (cpos < n), followed by the literal-only tail when the last match ends
   // before n (LZ4.c:585-612).  Rounds go on while a round is all matches.
-  // The block leaves as records -- sequence k: its match start | M << 9 |
-  // dist << 17 (its literal run starts where sequence k - 1's match ends; the
-  // tail is n | 0 | 0) -- after a header dword, the sum of the sequences'
-  // size fields | the sequence count << 16.  lz4_emit writes the bytes
+  // The block leaves as records -- sequence k: its match word dist | M << 9 |
+  // (match start + M) << 19 as the walk read it (its literal run starts where
+  // sequence k - 1's match ends; the tail is n << 19) -- after a header dword,
+  // the sum of the sequences' size fields | the sequence count << 16.  lz4_emit writes the bytes
   // (write_sequence / write_block, LZ4.c:365-425) straight into the stream.
   int nseq = 0;
   int ocar = 3;                      // block header: u8 nseq, u16 size
@@ -796,8 +813,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
     ws += M >= 19 ? 0x10001u : 0u;
     ws += (uint32_t)(M - 1) < 3u ? 0x10000u : 0u;
     const uint32_t tot = lane63(wave_incl_add(sel_mask(am, ws, 0u)));
-    if (sel_mask(am, 1u, 0u))
-      recs[1 + kk] = cq | (wv & 0x1FE00u) | ((wv & 511u) << 17);   // start | M | dist
+    if (sel_mask(am, 1u, 0u)) recs[1 + kk] = wv;   // the sequence's word (the tail: n << 19)
     ocar += (int)(tot & 0xFFFFu);
     szsum += (int)(tot >> 16);
     nseq += (int)__popcll(am);
@@ -1229,7 +1245,7 @@ __device__ __forceinline__ void encode_pair(uint8_t *__restrict__ L, const uint8
     const uint32_t totA = (uint32_t)__builtin_amdgcn_readlane((int)incl, 31);
     const uint32_t totB = lane63(incl) - totA;
     if (sel_mask(am, 1u, 0u))
-      recs[hf * (kSlot / 4) + 1 + kk] = (uint32_t)cq | (wv & 0x1FE00u) | ((wv & 511u) << 17);
+      recs[hf * (kSlot / 4) + 1 + kk] = wv - (hf ? 320u << 19 : 0u);
     ocarA += (int)(totA & 0xFFFFu);
     ocarB += (int)(totB & 0xFFFFu);
     hdrA = (totA >> 16) | ((uint32_t)__popcll(am & 0xFFFFFFFFull) << 16);
@@ -1274,7 +1290,7 @@ __device__ __forceinline__ void encode_pair(uint8_t *__restrict__ L, const uint8
         ws += (uint32_t)(M - 1) < 3u ? 0x10000u : 0u;
         const uint32_t tot = lane63(wave_incl_add(sel_mask(am, ws, 0u)));
         if (sel_mask(am, 1u, 0u))
-          recs[h * (kSlot / 4) + 1 + kq] = (uint32_t)cq | (wv & 0x1FE00u) | ((wv & 511u) << 17);
+          recs[h * (kSlot / 4) + 1 + kq] = wv - (h ? 320u << 19 : 0u);
         ocar += (int)(tot & 0xFFFFu);
         szsum += (int)(tot >> 16);
         nseq += (int)__popcll(am);
@@ -1620,9 +1636,11 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
         const int hb = bl0 + bi;
         const uint32_t *rp = reinterpret_cast<const uint32_t *>(wslots + (hb - h0) * kSlot);
         const uint32_t r = !valid ? 0u : (1 + k < kRecPre ? recst[hb - h0][1 + k] : rp[1 + k]);
-        const int cpos = (int)(r & 511u);
-        const int M = (int)((r >> 9) & 255u), D = (int)(r >> 17);
-        const int end = cpos + M;
+        // record = the sequence's match word: dist | M << 9 | (match start +
+        // M) << 19 (the literal tail: n << 19)
+        const int M = (int)((r >> 9) & 255u), D = (int)(r & 511u);
+        const int end = (int)(r >> 19);
+        const int cpos = end - M;
         const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
         const int pend = k == 0 ? 0 : (lane == 0 ? end_prev : (int)upv);   // literal run start
         end_prev = (int)lane63((uint32_t)end);
