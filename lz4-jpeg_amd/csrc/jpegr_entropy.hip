@@ -40,6 +40,12 @@
 
 #include "../../include/jpegr.h"
 
+// JPEGR_ENT_RLE_BRANCHY (tools A/B only): the round-3 count walk, a branch
+// per new / known symbol
+#ifndef JPEGR_ENT_RLE_BRANCHY
+#define JPEGR_ENT_RLE_BRANCHY 0
+#endif
+
 namespace {
 
 constexpr int kLanes = 64;
@@ -88,9 +94,11 @@ struct LCol {
   typedef T __attribute__((may_alias)) TA;
   typedef uint32_t __attribute__((may_alias)) WA;
   uint8_t *p;                                   // &block[0][lane] as bytes
+  // (indices are never negative: unsigned division is a shift and a mask)
   __device__ __forceinline__ TA &operator[](int i) const {
-    constexpr int per = 4 / (int)sizeof(T);
-    return *reinterpret_cast<TA *>(p + (i / per) * (4 * kLanes) + (i % per) * (int)sizeof(T));
+    constexpr uint32_t per = 4 / sizeof(T);
+    const uint32_t u = (uint32_t)i;
+    return *reinterpret_cast<TA *>(p + (u / per) * (4 * kLanes) + (u % per) * sizeof(T));
   }
   // zero elements [0, n) (n a multiple of 4 / sizeof(T)): whole dwords
   __device__ __forceinline__ void clear(int n) const {
@@ -106,6 +114,7 @@ struct LCol {
 // One lane's working set for a stream with at most Cap distinct symbols.
 template <template <typename> class A>
 struct Work {
+  static constexpr bool kPackLen = false;
   A<int16_t> sym;       // [Cap]       leaf -> symbol value (the int, without +1000)
   A<uint8_t> hash;      // [Hash]      open-addressing map symbol -> leaf + 1 (0 = empty)
   A<uint16_t> heap;     // [Cap + 2]   heap entry i (count << 8 | node id) at slot i + 1,
@@ -166,12 +175,13 @@ __device__ __forceinline__ uint16_t sift(const W &w, int size, int i, uint16_t x
 // trip, a done flag instead of a break.  Once x has landed, the remaining
 // levels rewrite x at its index (idempotent).  The loop form above paid the
 // exec-mask bookkeeping of every lane's own exit at every level.
-template <int Cap, class W>
-__device__ __forceinline__ uint16_t sift_fixed(const W &w, int size, int i, uint16_t x) {
+template <int Cap, int kDepth, class W>
+__device__ __forceinline__ uint16_t sift_depth(const W &w, int size, int i, uint16_t x) {
   constexpr int kMaxSlot = Cap & ~1;
-  constexpr int kDepth = Cap >= 16 ? 4 : Cap >= 8 ? 3 : Cap >= 4 ? 2 : 1;   // floor(log2 Cap)
-  static_assert(Cap <= 31, "fixed depth");
-  const int cx = x >> 8;
+  static_assert(Cap <= 31 && kDepth >= 1 && kDepth <= 4, "fixed depth");
+  // counts compare as whole entries against a count with a zero id byte
+  // (strict <): e < (c << 8) iff e >> 8 < c
+  const uint32_t xk = x & 0xFF00u;
   uint16_t top = x;
   bool done = false;
 #pragma unroll
@@ -181,12 +191,12 @@ __device__ __forceinline__ uint16_t sift_fixed(const W &w, int size, int i, uint
     const uint32_t pgl = w.heap.pair(min(2 * l + 2, kMaxSlot));  // l's children
     const uint32_t pgr = w.heap.pair(min(2 * l + 4, kMaxSlot));  // r's children
     {
-      const uint16_t hl = (uint16_t)pc, hr = (uint16_t)(pc >> 16);
-      const bool tl = l < size && (hl >> 8) < cx;
-      const int cs = tl ? (hl >> 8) : cx;
-      const bool tr = r < size && (hr >> 8) < cs;
+      const uint32_t hl = pc & 0xFFFFu, hr = pc >> 16;
+      const bool tl = l < size && hl < xk;
+      const uint32_t ck = tl ? (hl & 0xFF00u) : xk;
+      const bool tr = r < size && hr < ck;
       const bool mv = !done && (tl || tr);
-      const uint16_t hs = tr ? hr : hl;
+      const uint16_t hs = (uint16_t)(tr ? hr : hl);
       if (d == 0) top = mv ? hs : x;
       w.heap[i + 1] = mv ? hs : x;
       done = !mv;
@@ -195,18 +205,45 @@ __device__ __forceinline__ uint16_t sift_fixed(const W &w, int size, int i, uint
     if (d + 1 < kDepth) {
       const uint32_t pg = i == r ? pgr : pgl;                 // (unused once done)
       const int l2 = 2 * i + 1, r2 = l2 + 1;
-      const uint16_t gl = (uint16_t)pg, gr = (uint16_t)(pg >> 16);
-      const bool tl = l2 < size && (gl >> 8) < cx;
-      const int cs = tl ? (gl >> 8) : cx;
-      const bool tr = r2 < size && (gr >> 8) < cs;
+      const uint32_t gl = pg & 0xFFFFu, gr = pg >> 16;
+      const bool tl = l2 < size && gl < xk;
+      const uint32_t ck = tl ? (gl & 0xFF00u) : xk;
+      const bool tr = r2 < size && gr < ck;
       const bool mv = !done && (tl || tr);
-      w.heap[i + 1] = mv ? (tr ? gr : gl) : x;
+      w.heap[i + 1] = mv ? (uint16_t)(tr ? gr : gl) : x;
       done = !mv;
       i = mv ? (tr ? r2 : l2) : i;
     }
   }
   w.heap[i + 1] = x;
   return top;
+}
+
+template <int Cap, class W>
+__device__ __forceinline__ uint16_t sift_fixed(const W &w, int size, int i, uint16_t x) {
+  constexpr int kDepth = Cap >= 16 ? 4 : Cap >= 8 ? 3 : Cap >= 4 ? 2 : 1;   // floor(log2 Cap)
+  return sift_depth<Cap, kDepth>(w, size, i, x);
+}
+
+// The same with the depth cut to what a wave-uniform bound allows: no lane
+// of the wave sifts more than `levels` levels (a uniform branch picks the
+// unrolled depth).
+template <int Cap, class W>
+__device__ __forceinline__ uint16_t sift_levels(const W &w, int levels, int size, int i,
+                                                uint16_t x) {
+  if constexpr (Cap >= 16) {
+    if (levels >= 4) return sift_depth<Cap, 4>(w, size, i, x);
+  }
+  if (levels >= 3) return sift_depth<Cap, 3>(w, size, i, x);
+  if (levels == 2) return sift_depth<Cap, 2>(w, size, i, x);
+  return sift_depth<Cap, 1>(w, size, i, x);
+}
+
+// levels a sift from index i can descend in a heap of at most s entries
+__device__ __forceinline__ int sift_levels_bound(int s, int i) {
+  int d = 0;
+  for (int j = i; 2 * j + 1 < s; j = 2 * j + 1) ++d;
+  return d;
 }
 
 template <int Cap, class W>
@@ -224,9 +261,42 @@ __device__ __forceinline__ uint16_t sift_any(const W &w, int size, int i, uint16
 // order).  Returns true when a code exceeds the reference's char code[32].
 template <int Cap, class W>
 __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
-  for (int i = U / 2 - 1; i >= 0; --i) sift_any<Cap>(w, U, i, w.heap[i + 1]);
   int size = U, next = U;
-  uint16_t root = w.heap[1];
+  uint16_t root;
+  if constexpr (Cap <= 31) {
+    // Every lane's heap shrinks by one per merge, so at merge step t no lane's
+    // heap exceeds Umax - t (Umax: the wave's largest U): each sift runs only
+    // the levels that bound allows (and build_heap's sift from index i, the
+    // levels below i in a heap of Umax), picked by uniform branches.
+    int umax = 0;
+#pragma unroll
+    for (int b = 4; b >= 0; --b)
+      if (__ballot(U >= (umax | (1 << b)))) umax |= 1 << b;
+    for (int i = umax / 2 - 1; i >= 0; --i) {
+      const int lv = sift_levels_bound(umax, i);
+      if (i < U / 2) sift_levels<Cap>(w, lv, U, i, w.heap[i + 1]);
+    }
+    root = w.heap[1];
+    for (int t = 0; umax - t > 1; ++t) {
+      const int l1 = sift_levels_bound(umax - t - 1, 0), l2 = sift_levels_bound(umax - t - 2, 0);
+      if (size > 1) {
+        const uint16_t left = root;
+        --size;
+        root = sift_levels<Cap>(w, l1, size, 0, w.heap[size + 1]);
+        const uint16_t right = root;
+        --size;
+        root = sift_levels<Cap>(w, l2, size, 0, w.heap[size + 1]);
+        const uint16_t merged = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next);
+        w.heap[size + 1] = merged;                                              // not sifted up
+        w.heap[U - (next - U)] = (uint16_t)((left & 255) | ((right & 255) << 8));   // freed slot
+        ++size;
+        ++next;
+        if (size == 1) root = merged;
+      }
+    }
+  } else {
+  for (int i = U / 2 - 1; i >= 0; --i) sift_any<Cap>(w, U, i, w.heap[i + 1]);
+  root = w.heap[1];
   while (size > 1) {
     // pop, pop (the moved last entry sifted from the root; the new root is
     // known in registers), append the merged node unsifted
@@ -243,6 +313,7 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
     ++next;
     if (size == 1) root = merged;
   }
+  }
 
   // ---- codes: DFS, left first (JPEG.c:964-983) ------------------------------
   // Leaves pop in codes[] order; each code follows from the previous one:
@@ -252,22 +323,34 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
   int sp = 0, k = 0, plen = 0;
   uint32_t pcode = 0;
   int e = root & 255;                                 // the root, depth 0
+  // Both successors (the stack top, the node's children) and a leaf's symbol
+  // are read at the top of every step, one LDS round trip, so a leaf step
+  // does not wait on a second one before its table store.
   for (;;) {
     const int x = e & 255, d = e >> 8;
-    if (x < U) {                                      // leaf: next entry of codes[]
-      if (k) pcode = d >= plen ? (pcode + 1) << (d - plen) : (pcode + 1) >> (plen - d);
+    const bool leaf = x < U;
+    const int top = w.stk[sp > 0 ? sp - 1 : 0];       // a leaf's successor
+    const int ch = w.heap[leaf ? 0 : 2 * U - x];      // children of merged node x - U
+    const int sy = w.sym[leaf ? x : 0];               // a leaf's symbol
+    if (leaf) {                                       // leaf: next entry of codes[]
+      const uint32_t t = k ? pcode + 1 : 0u;
+      pcode = d >= plen ? t << (d - plen) : t >> (plen - d);
       plen = d;
-      w.code[x] = pcode;
-      w.len[x] = (uint8_t)d;
+      if constexpr (W::kPackLen) {
+        w.code[x] = pcode | (uint32_t)d << 24;        // depth <= Cap - 1 < 24
+      } else {
+        w.code[x] = pcode;
+        w.len[x] = (uint8_t)d;
+      }
       if (d > 31) over = true;                        // char code[32] (JPEG.c:861)
-      table[k++] = (uint16_t)w.sym[x] | ((uint32_t)d << 16);
-      if (sp == 0) break;
-      e = w.stk[--sp];
+      table[k] = (uint16_t)sy | ((uint32_t)d << 16);
     } else {
-      const int ch = w.heap[2 * U - x];               // children of merged node x - U
-      w.stk[sp++] = (uint16_t)((ch >> 8) | ((d + 1) << 8));   // right, visited later
-      e = (ch & 255) | ((d + 1) << 8);                         // left now
+      w.stk[sp] = (uint16_t)((ch >> 8) | ((d + 1) << 8));     // right, visited later
     }
+    if (leaf && sp == 0) break;
+    k += leaf ? 1 : 0;
+    sp += leaf ? -1 : 1;
+    e = leaf ? top : (ch & 255) | ((d + 1) << 8);              // left now
   }
   return over;
 }
@@ -418,8 +501,10 @@ struct LaneLds {
   static constexpr int Keys = N == 64 ? 176 : 120;   // symbols [-Off, Keys - Off)
   static constexpr int Off = N == 64 ? 64 : 48;       // counts: 1 .. N
   static constexpr int StkRows = (Cap + 2) / 2;       // overlays of the table (dword rows)
-  static constexpr int CodeRow = StkRows, LenRow = StkRows + Cap;
-  static_assert(LenRow + Cap / 4 <= Keys / 4, "stack, codes and lengths fit the table");
+  // a zero row, then code | length << 24 per leaf (leaf + 1 indexes from the
+  // zero row: id 0, no emission, reads a length-0 code)
+  static constexpr int ZeroRow = StkRows, CodeRow = StkRows + 1;
+  static_assert(CodeRow + Cap <= Keys / 4, "stack and codes fit the table");
   static_assert(Off + N < Keys, "every count is a key");
   uint32_t tab[Keys / 4][kLanes];
   uint32_t heap[(Cap + 2) / 2][kLanes];
@@ -427,10 +512,10 @@ struct LaneLds {
 };
 
 struct LaneWork {                                     // the arrays tree_codes uses
+  static constexpr bool kPackLen = true;              // code | length << 24, one read
   LCol<int8_t> sym;
   LCol<uint16_t> heap;
   LCol<uint32_t> code;
-  LCol<uint8_t> len;
   LCol<uint16_t> stk;
 };
 
@@ -450,8 +535,7 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   auto colp = [&](uint32_t *row0) { return reinterpret_cast<uint8_t *>(row0 + lane); };
   uint8_t *const tabc = colp(&S.tab[0][0]);
   const LaneWork w{{colp(&S.sym[0][0])}, {colp(&S.heap[0][0])},
-                   {colp(&S.tab[L::CodeRow][0])}, {colp(&S.tab[L::LenRow][0])},
-                   {colp(&S.tab[0][0])}};
+                   {colp(&S.tab[L::CodeRow][0])}, {colp(&S.tab[0][0])}};
 
   // the stream: N int16 as N / 2 packed dwords (16-B loads)
   uint32_t iw[N / 2];
@@ -481,6 +565,7 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   for (int j = 0; j < (N + 2) / 3; ++j) lid[j] = 0;
   int U = 0, start = 0;
   bool defer = false;
+#if JPEGR_ENT_RLE_BRANCHY
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int v = val(i);
@@ -524,6 +609,45 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
       }
     }
   }
+#else
+  // One exec region per position and no branch inside it: the stores are
+  // unconditional and idempotent (a known symbol rewrites its table entry and
+  // its symbol with the values they hold), and a count is a ds_add into the
+  // zeroed heap entry (a new leaf adds its id with its first count).  A
+  // stream that must be deferred runs on with clamped leaf ids over its own
+  // columns (the results are dropped).
+#pragma unroll
+  for (int r = 0; r < (Cap + 2) / 2; ++r) *heap_dw(2 * r) = 0u;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int v = val(i);
+    const bool end = i == N - 1 || val(i + 1 < N ? i + 1 : i) != v;
+    if (end) {
+      const int kc = i + 1 - start + Off;
+      start = i + 1;
+      const bool bad = (uint32_t)(v + Off) >= (uint32_t)Keys;
+      const int kv = bad ? kc : v + Off;
+      const int ec = tab_at(kc), ev = tab_at(kv);       // both reads in flight
+      const bool same = kv == kc;
+      const int lc = ec ? ec - 1 : U;
+      const int nu = U + (ec ? 0 : 1);
+      const int lv = same ? lc : (ev ? ev - 1 : nu);
+      const int nu2 = nu + ((same || ev) ? 0 : 1);
+      defer = defer || bad || nu2 > Cap;
+      const int lcw = min(lc, Cap - 1), lvw = min(lv, Cap - 1);
+      tab_at(kc) = (uint8_t)(lcw + 1);
+      tab_at(kv) = (uint8_t)(lvw + 1);
+      w.sym[lcw] = (int8_t)(kc - Off);
+      w.sym[lvw] = (int8_t)(kv - Off);
+      const uint32_t ac = (same ? 512u : 256u) | (ec ? 0u : (uint32_t)lcw);
+      const uint32_t av = same ? 0u : 256u | (ev ? 0u : (uint32_t)lvw);
+      atomicAdd(heap_dw(lcw + 1), ac << (16 * ((lcw + 1) & 1)));
+      atomicAdd(heap_dw(lvw + 1), av << (16 * ((lvw + 1) & 1)));
+      U = min(nu2, Cap);
+      lid[i / 3] |= (uint32_t)((lcw + 1) | ((lvw + 1) << 5)) << (10 * (i % 3));
+    }
+  }
+#endif
   if (defer) {
     const uint32_t slot = atomicAdd(&hdr->ndefer, 1u);
     deferred[slot] = (uint32_t)(tile * 3 + c);
@@ -540,28 +664,43 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   // ---- encoded sequence, MSB-first (JPEG.c:993-1007) ------------------------
   uint32_t *const wout = reinterpret_cast<uint32_t *>(bits + tile * kBitsPerTile + bits_off(c));
   constexpr int nwords = N / 2;                       // bits_cap / 32
+  // A leaf's code and length are one dword (code | length << 24); the reads
+  // do not depend on the bit accumulator, so each group of kG positions'
+  // code words is read while the previous group is shifted in.
+  const LCol<uint32_t> codez{colp(&S.tab[L::ZeroRow][0])};
+  codez[0] = 0u;
   uint64_t acc = 0;
-  int nacc = 0, nbits = 0, word = 0;
-  auto put = [&](int id) {                            // id = leaf + 1, 0: nothing
-    const int leaf = id ? id - 1 : 0;
-    const uint32_t cd = w.code[leaf];
-    const int Lb = id ? (int)w.len[leaf] : 0;
-    acc = (acc << Lb) | (id ? cd : 0u);
-    nacc += Lb;
-    nbits += Lb;
-    if (nacc >= 32) {
-      const uint32_t v = (uint32_t)(acc >> (nacc - 32));
-      if (word < nwords) wout[word] = __builtin_bswap32(v);
-      ++word;
-      nacc -= 32;
+  int nacc = 0, word = 0;
+  constexpr int kG = 4;
+  static_assert(N % kG == 0, "whole groups");
+  auto ident = [&](int i, int h) {                    // leaf + 1 of emission h at position i, 0: none
+    return (lid[i / 3] >> (10 * (i % 3) + 5 * h)) & 31u;
+  };
+  auto fetch = [&](int g, uint32_t (&cw)[2 * kG]) {
+#pragma unroll
+    for (int j = 0; j < 2 * kG; ++j) {
+      cw[j] = codez[(int)ident(g * kG + j / 2, j & 1)];
     }
   };
+  uint32_t cur[2 * kG], nxt[2 * kG];
+  fetch(0, nxt);
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const uint32_t id = (lid[i / 3] >> (10 * (i % 3))) & 1023u;
-    put((int)(id & 31u));
-    put((int)(id >> 5));
+  for (int g = 0; g < N / kG; ++g) {
+#pragma unroll
+    for (int j = 0; j < 2 * kG; ++j) cur[j] = nxt[j];
+    if (g + 1 < N / kG) fetch(g + 1, nxt);
+#pragma unroll
+    for (int j = 0; j < 2 * kG; ++j) {
+      const int Lb = (int)(cur[j] >> 24);
+      acc = (acc << Lb) | (cur[j] & 0xFFFFFFu);
+      nacc += Lb;
+      const bool full = nacc >= 32;
+      nacc -= full ? 32 : 0;
+      if (full && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc >> nacc));
+      word += full ? 1 : 0;
+    }
   }
+  const int nbits = 32 * word + nacc;
   if (nacc && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc << (32 - nacc)));
   if (nbits > ref_bits_max(c)) over = true;           // char sequence[1024] / [512]
   meta[tile * 3 + c] = (uint32_t)(nbits < 0xFFFF ? nbits : 0xFFFF) | ((uint32_t)R << 16) |
