@@ -37,14 +37,9 @@
 #include <stdint.h>
 
 #include <mutex>
+#include <type_traits>
 
 #include "../../include/jpegr.h"
-
-// JPEGR_ENT_RLE_BRANCHY (tools A/B only): the round-3 count walk, a branch
-// per new / known symbol
-#ifndef JPEGR_ENT_RLE_BRANCHY
-#define JPEGR_ENT_RLE_BRANCHY 0
-#endif
 
 namespace {
 
@@ -506,15 +501,38 @@ struct LaneLds {
   static constexpr int ZeroRow = StkRows, CodeRow = StkRows + 1;
   static_assert(CodeRow + Cap <= Keys / 4, "stack and codes fit the table");
   static_assert(Off + N < Keys, "every count is a key");
+  // Luma's heap takes a dword row per entry (no half-word address arithmetic
+  // in the sifts; 19 KB per wave, still 8 waves per CU: a 4K image's 2,025
+  // luma waves in one round); chroma's stays two entries per dword (10 KB:
+  // 16 waves per CU, its 4,050 waves in one round).
+  static constexpr bool Wide = N == 64;
+  static constexpr int HeapRows = Wide ? Cap + 2 : (Cap + 2) / 2;
+  static_assert(HeapRows >= Cap / 2, "the walk's (symbol | count) rows");
   uint32_t tab[Keys / 4][kLanes];
-  uint32_t heap[(Cap + 2) / 2][kLanes];
+  uint32_t heap[HeapRows][kLanes];
   uint32_t sym[Cap / 4][kLanes];                      // int8 symbols
 };
 
+// One lane's u16 array with an element per dword row (the low half); a pair
+// is two rows
+struct WCol {
+  typedef uint16_t __attribute__((may_alias)) TA;
+  typedef uint32_t __attribute__((may_alias)) WA;
+  uint8_t *p;
+  __device__ __forceinline__ TA &operator[](int i) const {
+    return *reinterpret_cast<TA *>(p + (uint32_t)i * (4 * kLanes));
+  }
+  __device__ __forceinline__ uint32_t pair(int i) const {
+    const WA *q = reinterpret_cast<const WA *>(p + (uint32_t)i * (4 * kLanes));
+    return __builtin_amdgcn_perm(q[kLanes], q[0], 0x05040100u);
+  }
+};
+
+template <class HeapCol>
 struct LaneWork {                                     // the arrays tree_codes uses
   static constexpr bool kPackLen = true;              // code | length << 24, one read
   LCol<int8_t> sym;
-  LCol<uint16_t> heap;
+  HeapCol heap;
   LCol<uint32_t> code;
   LCol<uint16_t> stk;
 };
@@ -534,8 +552,9 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   if (tile >= ntiles) return;
   auto colp = [&](uint32_t *row0) { return reinterpret_cast<uint8_t *>(row0 + lane); };
   uint8_t *const tabc = colp(&S.tab[0][0]);
-  const LaneWork w{{colp(&S.sym[0][0])}, {colp(&S.heap[0][0])},
-                   {colp(&S.tab[L::CodeRow][0])}, {colp(&S.tab[0][0])}};
+  using HeapCol = typename std::conditional<L::Wide, WCol, LCol<uint16_t>>::type;
+  const LaneWork<HeapCol> w{{colp(&S.sym[0][0])}, {colp(&S.heap[0][0])},
+                            {colp(&S.tab[L::CodeRow][0])}, {colp(&S.tab[0][0])}};
 
   // the stream: N int16 as N / 2 packed dwords (16-B loads)
   uint32_t iw[N / 2];
@@ -553,8 +572,8 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   auto tab_at = [&](int k) -> uint8_t & {
     return *(tabc + (k >> 2) * (4 * kLanes) + (k & 3));
   };
-  auto heap_dw = [&](int slot) {
-    return reinterpret_cast<uint32_t *>(w.heap.p + (slot >> 1) * (4 * kLanes));
+  auto row = [&](int r) {                            // dword row r of the heap rows
+    return reinterpret_cast<uint32_t *>(w.heap.p + r * (4 * kLanes));
   };
 
   // ---- RLE (JPEG.c:767-808) + frequencies (JPEG.c:864-886) ------------------
@@ -565,59 +584,14 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   for (int j = 0; j < (N + 2) / 3; ++j) lid[j] = 0;
   int U = 0, start = 0;
   bool defer = false;
-#if JPEGR_ENT_RLE_BRANCHY
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const int v = val(i);
-    const bool end = i == N - 1 || val(i + 1 < N ? i + 1 : i) != v;
-    if (end && !defer) {
-      const int kc = i + 1 - start + Off, kv = v + Off;
-      start = i + 1;
-      if ((uint32_t)kv >= (uint32_t)Keys) {
-        defer = true;
-      } else {
-        const int ec = tab_at(kc), ev = tab_at(kv);     // both reads in flight
-        const bool same = kv == kc;
-        const int lc = ec ? ec - 1 : U;
-        const int nu = U + (ec ? 0 : 1);
-        const int lv = same ? lc : (ev ? ev - 1 : nu);
-        const int nu2 = nu + ((same || ev) ? 0 : 1);
-        if (nu2 > Cap) {
-          defer = true;
-        } else {
-          // new leaves: table entry, symbol, heap entry (count << 8 | id);
-          // known ones: +1 on the count (ds_add on the entry's half-word)
-          if (!ec) {
-            tab_at(kc) = (uint8_t)(lc + 1);
-            w.sym[lc] = (int8_t)(kc - Off);
-            w.heap[lc + 1] = (uint16_t)(((same ? 2 : 1) << 8) | lc);
-          } else {
-            atomicAdd(heap_dw(lc + 1), (same ? 512u : 256u) << (16 * ((lc + 1) & 1)));
-          }
-          if (!same) {
-            if (!ev) {
-              tab_at(kv) = (uint8_t)(lv + 1);
-              w.sym[lv] = (int8_t)v;
-              w.heap[lv + 1] = (uint16_t)((1 << 8) | lv);
-            } else {
-              atomicAdd(heap_dw(lv + 1), 256u << (16 * ((lv + 1) & 1)));
-            }
-          }
-          U = nu2;
-          lid[i / 3] |= (uint32_t)((lc + 1) | ((lv + 1) << 5)) << (10 * (i % 3));
-        }
-      }
-    }
-  }
-#else
   // One exec region per position and no branch inside it: the stores are
   // unconditional and idempotent (a known symbol rewrites its table entry and
   // its symbol with the values they hold), and a count is a ds_add into the
-  // zeroed heap entry (a new leaf adds its id with its first count).  A
-  // stream that must be deferred runs on with clamped leaf ids over its own
-  // columns (the results are dropped).
+  // zeroed heap rows, which hold (symbol | count << 8) per leaf during the
+  // walk.  A stream that must be deferred runs on with clamped leaf ids over
+  // its own columns (the results are dropped).
 #pragma unroll
-  for (int r = 0; r < (Cap + 2) / 2; ++r) *heap_dw(2 * r) = 0u;
+  for (int r = 0; r < Cap / 2; ++r) *row(r) = 0u;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int v = val(i);
@@ -637,21 +611,47 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
       const int lcw = min(lc, Cap - 1), lvw = min(lv, Cap - 1);
       tab_at(kc) = (uint8_t)(lcw + 1);
       tab_at(kv) = (uint8_t)(lvw + 1);
-      w.sym[lcw] = (int8_t)(kc - Off);
-      w.sym[lvw] = (int8_t)(kv - Off);
-      const uint32_t ac = (same ? 512u : 256u) | (ec ? 0u : (uint32_t)lcw);
-      const uint32_t av = same ? 0u : 256u | (ev ? 0u : (uint32_t)lvw);
-      atomicAdd(heap_dw(lcw + 1), ac << (16 * ((lcw + 1) & 1)));
-      atomicAdd(heap_dw(lvw + 1), av << (16 * ((lvw + 1) & 1)));
+      // leaf u's symbol and count: one u16 (symbol | count << 8) at half
+      // u & 1 of dword row u >> 1, so the store and the add share an address
+      uint8_t *const sc = w.heap.p + ((lcw >> 1) << 8), *const sv = w.heap.p + ((lvw >> 1) << 8);
+      const int hc = (lcw & 1) << 4, hv = (lvw & 1) << 4;
+      sc[hc >> 3] = (uint8_t)(kc - Off);
+      sv[hv >> 3] = (uint8_t)(kv - Off);
+      atomicAdd(reinterpret_cast<uint32_t *>(sc), (same ? 2u : 1u) << (hc + 8));
+      atomicAdd(reinterpret_cast<uint32_t *>(sv), (same ? 0u : 1u) << (hv + 8));
       U = min(nu2, Cap);
       lid[i / 3] |= (uint32_t)((lcw + 1) | ((lvw + 1) << 5)) << (10 * (i % 3));
     }
   }
-#endif
   if (defer) {
     const uint32_t slot = atomicAdd(&hdr->ndefer, 1u);
     deferred[slot] = (uint32_t)(tile * 3 + c);
     return;
+  }
+  // (symbol | count << 8) per leaf -> the symbols (i8, 4 per dword) and the
+  // heap entries (count << 8 | leaf at slot leaf + 1)
+  {
+    uint32_t sc[Cap / 2];
+#pragma unroll
+    for (int k = 0; k < Cap / 2; ++k) sc[k] = *row(k);
+#pragma unroll
+    for (int j = 0; j < Cap / 4; ++j)
+      *reinterpret_cast<uint32_t *>(w.sym.p + j * (4 * kLanes)) =
+          __builtin_amdgcn_perm(sc[2 * j + 1], sc[2 * j], 0x06040200u);
+    if constexpr (L::Wide) {
+      // slot s (leaf s - 1) is row s
+#pragma unroll
+      for (int u = 0; u < Cap; ++u)
+        *row(u + 1) = ((sc[u >> 1] >> (16 * (u & 1))) & 0xFF00u) | (uint32_t)u;
+    } else {
+#pragma unroll
+      for (int r = 0; r < (Cap + 2) / 2; ++r) {
+        // slot 2r: leaf 2r - 1 (count: byte 3 of sc[r - 1]); slot 2r + 1: leaf 2r (byte 1 of sc[r])
+        const uint32_t lo = r > 0 ? (sc[r - 1] >> 16) & 0xFF00u : 0u;
+        const uint32_t hi = r < Cap / 2 ? (sc[r] & 0xFF00u) << 16 : 0u;
+        *row(r) = lo | hi | (uint32_t)(r > 0 ? 2 * r - 1 : 0) | (uint32_t)(2 * r) << 16;
+      }
+    }
   }
   int R = 0;
 #pragma unroll
