@@ -110,6 +110,7 @@ struct LCol {
 template <template <typename> class A>
 struct Work {
   static constexpr bool kPackLen = false;
+  static constexpr bool kWideRec = false;
   A<int16_t> sym;       // [Cap]       leaf -> symbol value (the int, without +1000)
   A<uint8_t> hash;      // [Hash]      open-addressing map symbol -> leaf + 1 (0 = empty)
   A<uint16_t> heap;     // [Cap + 2]   heap entry i (count << 8 | node id) at slot i + 1,
@@ -258,12 +259,12 @@ template <int Cap, class W>
 __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
   int size = U, next = U;
   uint16_t root;
+  int umax = 0;
   if constexpr (Cap <= 31) {
     // Every lane's heap shrinks by one per merge, so at merge step t no lane's
     // heap exceeds Umax - t (Umax: the wave's largest U): each sift runs only
     // the levels that bound allows (and build_heap's sift from index i, the
     // levels below i in a heap of Umax), picked by uniform branches.
-    int umax = 0;
 #pragma unroll
     for (int b = 4; b >= 0; --b)
       if (__ballot(U >= (umax | (1 << b)))) umax |= 1 << b;
@@ -283,7 +284,19 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
         root = sift_levels<Cap>(w, l2, size, 0, w.heap[size + 1]);
         const uint16_t merged = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next);
         w.heap[size + 1] = merged;                                              // not sifted up
-        w.heap[U - (next - U)] = (uint16_t)((left & 255) | ((right & 255) << 8));   // freed slot
+        if constexpr (W::kWideRec) {
+          // record of merged node next (row 2U - next, freed by the heap):
+          // left | right << 6 | leaves under it << 12 | leaves under left << 17
+          // (| DFS position << 22 | depth << 27, or-ed in top-down)
+          const int li = left & 255, ri = right & 255;
+          const uint32_t rl = *w.heap.word(li < U ? 0 : 2 * U - li);
+          const uint32_t rr = *w.heap.word(ri < U ? 0 : 2 * U - ri);
+          const uint32_t nl = li < U ? 1u : (rl >> 12) & 31u, nr = ri < U ? 1u : (rr >> 12) & 31u;
+          *w.heap.word(2 * U - next) =
+              (uint32_t)li | (uint32_t)ri << 6 | (nl + nr) << 12 | nl << 17;
+        } else {
+          w.heap[U - (next - U)] = (uint16_t)((left & 255) | ((right & 255) << 8));   // freed slot
+        }
         ++size;
         ++next;
         if (size == 1) root = merged;
@@ -315,6 +328,51 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
   // code[k] = (code[k-1] + 1) moved to length len[k].  The current node stays
   // in registers: an internal node stacks its right child and descends left.
   bool over = false;
+  if constexpr (W::kWideRec) {
+    // Top-down instead of the DFS: merged nodes from the root down (merge
+    // step t's node, id 2U - 2 - t, has its record in row t + 2 -- the same
+    // row in every lane), each handing its children their depth and DFS
+    // position (left: the parent's; right: + the leaves under left); a leaf
+    // records (depth | leaf << 8) at its position in the retired stack rows.
+    // U - 1 steps instead of 2U - 1, and the records' reads are uniform rows.
+    // Then the leaves in DFS order give the codes as the DFS does.
+    if (U == 1) w.stk[0] = 0;                         // the root is leaf 0, depth 0
+    for (int t = 0; t + 1 < umax; ++t) {
+      if (t + 1 < U) {
+        const uint32_t rc = *w.heap.word(t + 2);
+        const int li = (int)(rc & 63u), ri = (int)((rc >> 6) & 63u);
+        const uint32_t pos = (rc >> 22) & 31u, dc = (rc >> 27) + 1u, nl = (rc >> 17) & 31u;
+        if (li < U) w.stk[(int)pos] = (uint16_t)(dc | (uint32_t)li << 8);
+        else atomicOr(w.heap.word(2 * U - li), pos << 22 | dc << 27);
+        if (ri < U) w.stk[(int)(pos + nl)] = (uint16_t)(dc | (uint32_t)ri << 8);
+        else atomicOr(w.heap.word(2 * U - ri), (pos + nl) << 22 | dc << 27);
+      }
+    }
+    int plen = 0;
+    uint32_t pcode = 0;
+    uint32_t de[Cap];
+    int sy[Cap];
+#pragma unroll
+    for (int k = 0; k < Cap; ++k)
+      if (k < umax) de[k] = w.stk[k];
+#pragma unroll
+    for (int k = 0; k < Cap; ++k)
+      if (k < umax) sy[k] = w.sym[min((int)(de[k] >> 8), Cap - 1)];
+#pragma unroll
+    for (int k = 0; k < Cap; ++k) {
+      if (k < umax) {
+        const int d = (int)(de[k] & 255u), x = min((int)(de[k] >> 8), Cap - 1);
+        const uint32_t t = k ? pcode + 1 : 0u;
+        pcode = d >= plen ? t << (d - plen) : t >> (plen - d);
+        plen = d;
+        if (k < U) {
+          w.code[x] = pcode | (uint32_t)d << 24;      // depth <= Cap - 1 < 24
+          table[k] = (uint16_t)sy[k] | ((uint32_t)d << 16);
+        }
+      }
+    }
+    return over;
+  }
   int sp = 0, k = 0, plen = 0;
   uint32_t pcode = 0;
   int e = root & 255;                                 // the root, depth 0
@@ -526,11 +584,18 @@ struct WCol {
     const WA *q = reinterpret_cast<const WA *>(p + (uint32_t)i * (4 * kLanes));
     return __builtin_amdgcn_perm(q[kLanes], q[0], 0x05040100u);
   }
+  // the whole dword of row i
+  __device__ __forceinline__ uint32_t *word(int i) const {
+    return reinterpret_cast<uint32_t *>(p + (uint32_t)i * (4 * kLanes));
+  }
 };
 
 template <class HeapCol>
 struct LaneWork {                                     // the arrays tree_codes uses
   static constexpr bool kPackLen = true;              // code | length << 24, one read
+  // dword heap rows: a merged node's record has room for the top-down code
+  // assignment's fields (tree_codes)
+  static constexpr bool kWideRec = std::is_same<HeapCol, WCol>::value;
   LCol<int8_t> sym;
   HeapCol heap;
   LCol<uint32_t> code;
