@@ -32,6 +32,13 @@ namespace {
 
 constexpr int kTiles = 32;       // tiles per workgroup strip
 constexpr int kThreads = 256;    // 4 waves
+// the encoder's strip (JPEGR_STRIP_TILES: tools A/B of a narrower strip)
+#ifndef JPEGR_STRIP_TILES
+#define JPEGR_STRIP_TILES 32
+#endif
+constexpr int kETiles = JPEGR_STRIP_TILES;
+constexpr int kEThreads = 8 * kETiles;   // thread = (tile, row u)
+static_assert(kETiles == 16 || kETiles == 32, "strip of 16 or 32 tiles");
 constexpr int kYStride = 66;     // doubles per Y tile in LDS (528 B: bank skew 4)
 constexpr int kCStride = 34;     // doubles per chroma tile (272 B: bank skew 4)
 
@@ -136,34 +143,34 @@ __device__ __forceinline__ void quantize_row(const double (&cf)[W], const int *T
 }
 
 template <bool RAW>
-__global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
+__global__ __launch_bounds__(kEThreads) void jpeg_strip_kernel(
     const uint8_t *__restrict__ rgba, int w, int h, int tiles_x, int tiles_y,
     int strips, void *__restrict__ out) {
   // 16-B aligned: phase 4 reads the int16 output staged over it as uint4
-  __shared__ alignas(16) double ylds[kTiles * kYStride];
-  __shared__ double crl[kTiles * kCStride];
-  __shared__ double cbl[kTiles * kCStride];
+  __shared__ alignas(16) double ylds[kETiles * kYStride];
+  __shared__ double crl[kETiles * kCStride];
+  __shared__ double cbl[kETiles * kCStride];
   // the strip's int16 output is staged over the luma samples once every
   // thread holds its coefficients in registers (34 KB of LDS: 4 WGs per CU)
   int16_t *const olds = reinterpret_cast<int16_t *>(ylds);
 
   const int img = blockIdx.y;
   const int br = blockIdx.x / strips;
-  const int bc0 = (blockIdx.x - br * strips) * kTiles;
-  const int ntiles = min(kTiles, tiles_x - bc0);
+  const int bc0 = (blockIdx.x - br * strips) * kETiles;
+  const int ntiles = min(kETiles, tiles_x - bc0);
   const size_t img_px = (size_t)w * (size_t)h;
   const uint8_t *src = rgba + (size_t)img * img_px * 4;
   const int t = threadIdx.x;
 
   // ---- phase 1: colour conversion into LDS --------------------------------
   {
-    const int r = t >> 5;           // tile row 0..7
-    const int c = t & 31;
+    const int r = t / kETiles;      // tile row 0..7
+    const int c = t % kETiles;
     const int row = br * 8 + r;
     const bool row_ok = row < h;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      const int lx = half * 128 + c * 4;   // pixel column within the strip
+      const int lx = half * (4 * kETiles) + c * 4;   // pixel column within the strip
       const int x = bc0 * 8 + lx;
       uint32_t p[4];
       bool ok[4];
@@ -268,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_strip_kernel(
     const int bytes = ntiles * 256;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const int off = (k * kThreads + t) * 16;
+      const int off = (k * kEThreads + t) * 16;
       if (off < bytes)
         *reinterpret_cast<uint4 *>(dst + off) =
             *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(olds) + off);
@@ -492,16 +499,16 @@ int launch(bool raw, const void *d_rgba, int w, int h, int nimg, void *d_out,
     return JPEGR_ERR_ARG;
   if (upload_tables() != hipSuccess) return JPEGR_ERR_HIP;
   const int tx = (w + 7) / 8, ty = (h + 7) / 8;
-  const int strips = (tx + kTiles - 1) / kTiles;
+  const int strips = (tx + kETiles - 1) / kETiles;
   const long long gx = (long long)ty * strips;
   if (gx > 0x7fffffffLL) return JPEGR_ERR_ARG;
   dim3 grid((unsigned)gx, (unsigned)nimg);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (raw)
-    hipLaunchKernelGGL(jpeg_strip_kernel<true>, grid, dim3(kThreads), 0, s,
+    hipLaunchKernelGGL(jpeg_strip_kernel<true>, grid, dim3(kEThreads), 0, s,
                        static_cast<const uint8_t *>(d_rgba), w, h, tx, ty, strips, d_out);
   else
-    hipLaunchKernelGGL(jpeg_strip_kernel<false>, grid, dim3(kThreads), 0, s,
+    hipLaunchKernelGGL(jpeg_strip_kernel<false>, grid, dim3(kEThreads), 0, s,
                        static_cast<const uint8_t *>(d_rgba), w, h, tx, ty, strips, d_out);
   return hipGetLastError() == hipSuccess ? JPEGR_OK : JPEGR_ERR_HIP;
 }

@@ -110,7 +110,7 @@ struct LCol {
 template <template <typename> class A>
 struct Work {
   static constexpr bool kPackLen = false;
-  static constexpr bool kWideRec = false;
+  static constexpr bool kTopDown = false;
   A<int16_t> sym;       // [Cap]       leaf -> symbol value (the int, without +1000)
   A<uint8_t> hash;      // [Hash]      open-addressing map symbol -> leaf + 1 (0 = empty)
   A<uint16_t> heap;     // [Cap + 2]   heap entry i (count << 8 | node id) at slot i + 1,
@@ -284,16 +284,14 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
         root = sift_levels<Cap>(w, l2, size, 0, w.heap[size + 1]);
         const uint16_t merged = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next);
         w.heap[size + 1] = merged;                                              // not sifted up
-        if constexpr (W::kWideRec) {
-          // record of merged node next (row 2U - next, freed by the heap):
-          // left | right << 6 | leaves under it << 12 | leaves under left << 17
-          // (| DFS position << 22 | depth << 27, or-ed in top-down)
+        if constexpr (W::kTopDown) {
+          // record of merged node m = next - U: left | right << 6 | leaves
+          // under it << 12 | leaves under left << 17 (| DFS position << 22 |
+          // depth << 27, or-ed in top-down)
           const int li = left & 255, ri = right & 255;
-          const uint32_t rl = *w.heap.word(li < U ? 0 : 2 * U - li);
-          const uint32_t rr = *w.heap.word(ri < U ? 0 : 2 * U - ri);
+          const uint32_t rl = w.mrec[li < U ? 0 : li - U], rr = w.mrec[ri < U ? 0 : ri - U];
           const uint32_t nl = li < U ? 1u : (rl >> 12) & 31u, nr = ri < U ? 1u : (rr >> 12) & 31u;
-          *w.heap.word(2 * U - next) =
-              (uint32_t)li | (uint32_t)ri << 6 | (nl + nr) << 12 | nl << 17;
+          w.mrec[next - U] = (uint32_t)li | (uint32_t)ri << 6 | (nl + nr) << 12 | nl << 17;
         } else {
           w.heap[U - (next - U)] = (uint16_t)((left & 255) | ((right & 255) << 8));   // freed slot
         }
@@ -328,24 +326,24 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
   // code[k] = (code[k-1] + 1) moved to length len[k].  The current node stays
   // in registers: an internal node stacks its right child and descends left.
   bool over = false;
-  if constexpr (W::kWideRec) {
+  if constexpr (W::kTopDown) {
     // Top-down instead of the DFS: merged nodes from the root down (merge
-    // step t's node, id 2U - 2 - t, has its record in row t + 2 -- the same
-    // row in every lane), each handing its children their depth and DFS
-    // position (left: the parent's; right: + the leaves under left); a leaf
-    // records (depth | leaf << 8) at its position in the retired stack rows.
-    // U - 1 steps instead of 2U - 1, and the records' reads are uniform rows.
-    // Then the leaves in DFS order give the codes as the DFS does.
-    if (U == 1) w.stk[0] = 0;                         // the root is leaf 0, depth 0
+    // step t's node is m = U - 2 - t), each handing its children their depth
+    // and DFS position (left: the parent's; right: + the leaves under left);
+    // a leaf records (depth | leaf << 8) at its position.  U - 1 steps
+    // instead of 2U - 1.  Then the leaves in DFS order give the codes as the
+    // DFS does.
+    static_assert(2 * Cap - 1 <= 64 && Cap <= 31, "record fields");
+    if (U == 1) w.dep[0] = 0;                         // the root is leaf 0, depth 0
     for (int t = 0; t + 1 < umax; ++t) {
       if (t + 1 < U) {
-        const uint32_t rc = *w.heap.word(t + 2);
+        const uint32_t rc = w.mrec[U - 2 - t];
         const int li = (int)(rc & 63u), ri = (int)((rc >> 6) & 63u);
         const uint32_t pos = (rc >> 22) & 31u, dc = (rc >> 27) + 1u, nl = (rc >> 17) & 31u;
-        if (li < U) w.stk[(int)pos] = (uint16_t)(dc | (uint32_t)li << 8);
-        else atomicOr(w.heap.word(2 * U - li), pos << 22 | dc << 27);
-        if (ri < U) w.stk[(int)(pos + nl)] = (uint16_t)(dc | (uint32_t)ri << 8);
-        else atomicOr(w.heap.word(2 * U - ri), (pos + nl) << 22 | dc << 27);
+        if (li < U) w.dep[(int)pos] = (uint16_t)(dc | (uint32_t)li << 8);
+        else atomicOr(&w.mrec[li - U], pos << 22 | dc << 27);
+        if (ri < U) w.dep[(int)(pos + nl)] = (uint16_t)(dc | (uint32_t)ri << 8);
+        else atomicOr(&w.mrec[ri - U], (pos + nl) << 22 | dc << 27);
       }
     }
     int plen = 0;
@@ -354,7 +352,7 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
     int sy[Cap];
 #pragma unroll
     for (int k = 0; k < Cap; ++k)
-      if (k < umax) de[k] = w.stk[k];
+      if (k < umax) de[k] = w.dep[k];
 #pragma unroll
     for (int k = 0; k < Cap; ++k)
       if (k < umax) sy[k] = w.sym[min((int)(de[k] >> 8), Cap - 1)];
@@ -372,7 +370,7 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
       }
     }
     return over;
-  }
+  } else {
   int sp = 0, k = 0, plen = 0;
   uint32_t pcode = 0;
   int e = root & 255;                                 // the root, depth 0
@@ -406,6 +404,7 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
     e = leaf ? top : (ch & 255) | ((d + 1) << 8);              // left now
   }
   return over;
+  }
 }
 
 enum : int { kOk = 0, kDefer = 1, kOverflow = 2 };
@@ -558,6 +557,9 @@ struct LaneLds {
   // zero row: id 0, no emission, reads a length-0 code)
   static constexpr int ZeroRow = StkRows, CodeRow = StkRows + 1;
   static_assert(CodeRow + Cap <= Keys / 4, "stack and codes fit the table");
+  // (the merge records, Cap - 1 rows from row 0, are dead before the codes
+  // and the zero row are written; the depths by DFS position take Cap / 2
+  // rows of the dead heap)
   static_assert(Off + N < Keys, "every count is a key");
   // Luma's heap takes a dword row per entry (no half-word address arithmetic
   // in the sifts; 19 KB per wave, still 8 waves per CU: a 4K image's 2,025
@@ -584,22 +586,17 @@ struct WCol {
     const WA *q = reinterpret_cast<const WA *>(p + (uint32_t)i * (4 * kLanes));
     return __builtin_amdgcn_perm(q[kLanes], q[0], 0x05040100u);
   }
-  // the whole dword of row i
-  __device__ __forceinline__ uint32_t *word(int i) const {
-    return reinterpret_cast<uint32_t *>(p + (uint32_t)i * (4 * kLanes));
-  }
 };
 
 template <class HeapCol>
 struct LaneWork {                                     // the arrays tree_codes uses
   static constexpr bool kPackLen = true;              // code | length << 24, one read
-  // dword heap rows: a merged node's record has room for the top-down code
-  // assignment's fields (tree_codes)
-  static constexpr bool kWideRec = std::is_same<HeapCol, WCol>::value;
+  static constexpr bool kTopDown = true;              // codes top-down over mrec (tree_codes)
   LCol<int8_t> sym;
   HeapCol heap;
   LCol<uint32_t> code;
-  LCol<uint16_t> stk;
+  LCol<uint32_t> mrec;   // merged node m's record (the dead table's rows, before the codes)
+  LCol<uint16_t> dep;    // (depth | leaf << 8) by DFS position (the dead heap's rows)
 };
 
 template <bool kLuma>
@@ -619,7 +616,8 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   uint8_t *const tabc = colp(&S.tab[0][0]);
   using HeapCol = typename std::conditional<L::Wide, WCol, LCol<uint16_t>>::type;
   const LaneWork<HeapCol> w{{colp(&S.sym[0][0])}, {colp(&S.heap[0][0])},
-                            {colp(&S.tab[L::CodeRow][0])}, {colp(&S.tab[0][0])}};
+                            {colp(&S.tab[L::CodeRow][0])}, {colp(&S.tab[0][0])},
+                            {colp(&S.heap[0][0])}};
 
   // the stream: N int16 as N / 2 packed dwords (16-B loads)
   uint32_t iw[N / 2];
