@@ -399,6 +399,21 @@ __device__ __forceinline__ uint32_t sel_mask(uint64_t m, uint32_t t, uint32_t f)
   return r;
 }
 
+// base[1 + off / 4] = v in the lanes of m: EXEC = EXEC & m around one
+// global_store_dword, straight from the SGPR pair (a condition built from the
+// mask costs a 0/1 select and a compare per store).  The untracked store only
+// makes the compiler's later vmcnt waits conservative.
+__device__ __forceinline__ void store_lanes1(uint64_t m, uint32_t *base, uint32_t off, uint32_t v) {
+  uint64_t save;
+  asm volatile(
+      "s_and_saveexec_b64 %0, %1\n\t"
+      "global_store_dword %2, %3, %4 offset:4\n\t"
+      "s_or_b64 exec, exec, %0"
+      : "=&s"(save)
+      : "s"(m), "v"(off), "v"(v), "s"(base)
+      : "memory", "scc");
+}
+
 // The compressor's workgroup is one wave.  A wave's LDS operations are
 // served in order, so its phase boundaries need neither s_barrier nor the
 // s_waitcnt vmcnt(0) lgkmcnt(0) that __syncthreads() implies: a compiler
@@ -813,7 +828,7 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
     ws += M >= 19 ? 0x10001u : 0u;
     ws += (uint32_t)(M - 1) < 3u ? 0x10000u : 0u;
     const uint32_t tot = lane63(wave_incl_add(sel_mask(am, ws, 0u)));
-    if (sel_mask(am, 1u, 0u)) recs[1 + kk] = wv;   // the sequence's word (the tail: n << 19)
+    store_lanes1(am, recs, 4u * (uint32_t)kk, wv);   // recs[1 + kk]: the sequence's word (the tail: n << 19)
     ocar += (int)(tot & 0xFFFFu);
     szsum += (int)(tot >> 16);
     nseq += (int)__popcll(am);
