@@ -82,6 +82,17 @@ def test_batch_equals_singles(gpu, oracle):
         assert (got[i] == oracle.jpeg_encode(imgs[i])).all()
 
 
+def test_batch_odd_strip_count(gpu, oracle):
+    # a multi-image launch runs two strips per workgroup: 3 strips per image
+    # (one 25-tile strip per tile row) leaves each image's last workgroup one
+    from lz4jpeg import synth
+    imgs = np.stack([synth.rand_rgba(200, 24, seed=s) for s in (7, 8, 9)])
+    got = _enc(imgs, nimg=3).reshape(3, -1)
+    for i in range(3):
+        assert (got[i] == oracle.jpeg_encode(imgs[i])).all()
+        assert (got[i] == _enc(imgs[i])).all()
+
+
 def test_host_api(gpu, oracle):
     from lz4jpeg import jpeg, synth
     img = synth.rand_rgba(120, 80, seed=5)
