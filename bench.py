@@ -194,7 +194,7 @@ def maybe_self_launch(args, argv, env=None):
     (this process never touches the GPU; a process that has may not exec) and
     return their exit status.  None when this process is a rank itself."""
     env = os.environ if env is None else env
-    if args.gpus <= 1 or "WORLD_SIZE" in env:
+    if (args.gpus <= 1 and not getattr(args, "dist", False)) or "WORLD_SIZE" in env:
         return None
     cmd = launcher_cmd(args.gpus, argv, _free_port())
     log("launching", args.gpus, "ranks:", " ".join(cmd[2:]))
@@ -211,7 +211,7 @@ def rank_env(env=None):
 
 def workloads(world, args):
     """(lz4 bytes in total, jpeg images in total, scaling) for this job."""
-    if world == 1:
+    if world == 1 and not getattr(args, "dist", False):
         return args.lz4_bytes_per_rank, args.jpeg_images_per_rank, "weak"
     total = args.lz4_total_bytes or CFG4_BYTES
     imgs = args.jpeg_total_images or CFG5_IMAGES
@@ -262,6 +262,10 @@ def main(argv=None):
                     help="skip the 128-image single-launch JPEG line at N = 1")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target wall time of the all-core CPU-baseline sample")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the N > 1 code path (RCCL process group, sharded config-4/5 "
+                         "workloads, length all_gather, gatherv) even at one rank: the "
+                         "world-size-1 rehearsal of the 8-GPU job")
     ap.add_argument("--launch-check", action="store_true",
                     help="print each rank's (rank, world, local rank, shares) and exit "
                          "without touching the GPU (tests the launcher plumbing)")
@@ -288,9 +292,10 @@ def main(argv=None):
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    multi = world > 1 or args.dist       # the distributed code path
+    if multi:
         dist.init_process_group("nccl", device_id=dev)
-    ctx = Ctx(world, rank, dev, args, torch, dist)
+    ctx = Ctx(world, rank, dev, args, torch, dist, multi)
     lz4_total, jpeg_total, scaling = workloads(world, args)
 
     line = run_lz4(ctx, lz4_total, scaling)
@@ -299,37 +304,40 @@ def main(argv=None):
     else:
         line["jpeg"] = None
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not multi and not args.no_cpu_baseline:
         cpu_lz4, cpu_jpeg = cpu_baselines(ctx.host_text, args, ctx.host_img)
         line["cpu_baseline"] = cpu_lz4
         if line["jpeg"] is not None:
             line["jpeg"]["cpu_baseline"] = cpu_jpeg
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 
 class Ctx:
-    def __init__(self, world, rank, dev, args, torch, dist):
+    def __init__(self, world, rank, dev, args, torch, dist, multi=None):
         self.world, self.rank, self.dev, self.args = world, rank, dev, args
         self.torch, self.dist = torch, dist
+        # the distributed code path (a process group exists): world > 1, or the
+        # --dist rehearsal at one rank
+        self.multi = world > 1 if multi is None else multi
         self.host_text = None
         self.host_img = None
 
     def barrier(self):
-        if self.world > 1:
+        if self.multi:
             self.dist.barrier()
 
     def max_over_ranks(self, x):
-        if self.world == 1:
+        if not self.multi:
             return x
         t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum_over_ranks(self, x):
-        if self.world == 1:
+        if not self.multi:
             return x
         t = self.torch.tensor([x], dtype=self.torch.int64, device=self.dev)
         self.dist.all_reduce(t)
@@ -346,7 +354,7 @@ def run_lz4(ctx, n_total, scaling):
     n = hi - lo
     final_shard = hi == n_total
     log(f"rank {rank}: synthesising LZ4 shard [{lo}, {hi}) of {n_total} B in HBM")
-    if rank == 0 and world == 1:
+    if rank == 0 and not ctx.multi:
         # bounded host copy for the CPU baseline (the same bytes); made before
         # the device input so that seconds of host work do not sit between the
         # device synthesis and the warm-up steps (the clock ramps back up over
@@ -362,11 +370,14 @@ def run_lz4(ctx, n_total, scaling):
     stream = torch.cuda.current_stream()
 
     def lz4_step():
-        if world == 1:
+        if not ctx.multi:
             _, got = comp.compress_device(d_in, n, d_out)
             return got
         comp.compress_async(d_in, n, d_out[1:], d_len, segment=True, final_shard=final_shard)
-        seg = comp.async_length(d_len)
+        # the raw signed length (negative: a corrupt LDS index); exchange_lengths
+        # gathers it first and then raises on every rank (raising here would
+        # leave the other ranks waiting in the collective)
+        seg = int(d_len.item())
         ldist.exchange_lengths(seg, dev)
         return seg
 
@@ -399,7 +410,7 @@ def run_lz4(ctx, n_total, scaling):
     lz4_gbs = n_total / (dt / args.steps) / 1e9
     avg_match_ms = ctx.max_over_ranks(sum(match_ms) / len(match_ms))
     avg_call_ms = ctx.max_over_ranks(sum(call_ms) / len(call_ms))
-    out_total = ctx.sum_over_ranks(out_len) + (1 if world > 1 else 0)
+    out_total = ctx.sum_over_ranks(out_len) + (1 if ctx.multi else 0)
     log(f"lz4: {lz4_ms:.3f} ms/step, {lz4_gbs:.1f} GB/s aggregate, lz4_tiles "
         f"{avg_match_ms:.3f} ms, call {avg_call_ms:.3f} ms, out {out_total} B; step wall "
         f"min/median/max {min(step_ms):.3f}/{sorted(step_ms)[len(step_ms) // 2]:.3f}/"
@@ -408,7 +419,7 @@ def run_lz4(ctx, n_total, scaling):
     # decoder: this rank's blocks -> bytes, in HBM, with the
     # compressor's device-resident block offsets (no host round trip)
     nb_local = ldist.nblocks(n)
-    if world == 1:
+    if not ctx.multi:
         _, flen = comp.compress_device(d_in, n, d_out)
     else:
         comp.compress_async(d_in, n, d_out[1:], d_len, segment=True, final_shard=final_shard)
@@ -478,9 +489,9 @@ def run_lz4(ctx, n_total, scaling):
 
     # N > 1: assemble the framed stream on rank 0 (RCCL gatherv over xGMI)
     gather_ms = gather_ok = None
-    if world > 1:
+    if ctx.multi:
         comp.compress_async(d_in, n, d_out[1:], d_len, segment=True, final_shard=final_shard)
-        seg = comp.async_length(d_len)
+        seg = int(d_len.item())              # raw: exchange_lengths raises on every rank
         lens, offs = ldist.exchange_lengths(seg, dev)
         torch.cuda.synchronize()
         ctx.barrier()
@@ -501,7 +512,7 @@ def run_lz4(ctx, n_total, scaling):
     # compress and its length read back (the all_gather of one rank is that
     # read) -- so the driver's 1 -> 8 curve has a same-work denominator
     share = None
-    if world == 1 and not args.no_cfg4_share:
+    if not ctx.multi and not args.no_cfg4_share:
         share = run_cfg4_share(ctx, comp)
 
     roof_lz4 = {
@@ -526,11 +537,11 @@ def run_lz4(ctx, n_total, scaling):
                 "(DESIGN.md), not HBM-bound",
     }
     comp.close()
-    cfg = ("lz4_compress_1GiB_text_per_gpu" if world == 1 else
+    cfg = ("lz4_compress_1GiB_text_per_gpu" if not ctx.multi else
            "lz4_compress_64GiB_text_sharded_rccl_gather")
-    if world == 1 and n != 1 << 30:
+    if not ctx.multi and n != 1 << 30:
         cfg = f"lz4_compress_{n}B_text_per_gpu"
-    if world > 1 and n_total != CFG4_BYTES:
+    if ctx.multi and n_total != CFG4_BYTES:
         cfg = f"lz4_compress_{n_total}B_text_sharded_rccl_gather"
     return {
         "metric": "LZ4 compress GB/s + JPEG DCT Mpixel/s at 1/2/4/8 MI355X; % HBM roofline",
@@ -541,7 +552,7 @@ def run_lz4(ctx, n_total, scaling):
                 "newlines->spaces, glibc rand seed 1; each rank synthesises its shard in HBM",
         "config": {"workload": cfg, "bytes_per_rank": n, "bytes_total": n_total, "block": 300,
                    "parallelism": f"shard{world}", "compressed_bytes_total": out_total,
-                   "step": ("compress" if world == 1 else
+                   "step": ("compress" if not ctx.multi else
                             "segment compress + all_gather of segment lengths")},
         "roofline": roof_lz4,
         "cpu_baseline": None,
@@ -617,7 +628,7 @@ def run_jpeg(ctx, total_images, scaling):
     # image k = pixels [k W H, (k + 1) W H)
     d_img = torch.empty(4 * px * B, dtype=torch.uint8, device=dev)
     synth.rand_rgba_device(d_img, i0 * px, px * B, seed=1)
-    if rank == 0 and world == 1:
+    if rank == 0 and not ctx.multi:
         ctx.host_img = synth.rand_rgba_stream(0, px, 1).reshape(H, W, 4)
     d_coef = torch.empty(B * jpeg.coef_count(W, H), dtype=torch.int16, device=dev)
     jsteps = args.jpeg_steps or (max(50, 10 * args.steps) if B == 1 else max(5, args.steps))
@@ -641,7 +652,7 @@ def run_jpeg(ctx, total_images, scaling):
     gpix = px_total / (jdt / jsteps) / 1e9
     px_rank = px * B
     tiles = ((W + 7) // 8) * ((H + 7) // 8) * B
-    if world == 1:
+    if not ctx.multi:
         wl = "jpeg_encode_3840x2160_rgb" if (W, H, B) == (W4K, H4K, 1) else f"jpeg_encode_{B}x{W}x{H}"
     else:
         wl = (f"jpeg_encode_{total_images}x{W}x{H}_rand_stream" if (W, H) != (W4K, H4K) or
@@ -670,8 +681,7 @@ def run_jpeg(ctx, total_images, scaling):
                 "peak": FP64_VALU_PEAK_TOPS,
                 "frac": round(tiles * 13312 / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
                 **at_held_clock(tiles * 13312 / (kern_ms / 1e3) / 1e12, FP64_VALU_PEAK_TOPS,
-                                ["jpeg:void jpeg_strip_kernel<false, 1>",
-                                 "jpeg:void jpeg_strip_kernel<false>"]),
+                                ["jpeg:void jpeg_strip_kernel<false>"]),
                 "note": "13312 non-fused fp64 mul/add per tile in reference order "
                         "(8704 luma + 2x2304 chroma); peak = 78.6 TF fp64 vector spec / 2 at "
                         "2.4 GHz; peak_at_held_clock = the same per cycle at the clock the "
@@ -683,7 +693,7 @@ def run_jpeg(ctx, total_images, scaling):
     }
     log(f"jpeg: {jres['ms_per_step']} ms/step, {gpix:.2f} Gpix/s aggregate, kernel {kern_ms:.4f} ms")
 
-    if world == 1 and B == 1 and not args.no_jpeg_batch:
+    if not ctx.multi and B == 1 and not args.no_jpeg_batch:
         # config 5's per-GPU share at 8 GPUs (images 0..127 of the stream) in one
         # launch: the single-image line above pays the launch ramp and drain once
         # per 4K image
@@ -715,8 +725,7 @@ def run_jpeg(ctx, total_images, scaling):
                 "achieved": round(btiles * 13312 / (bms / 1e3) / 1e12, 2),
                 "frac": round(btiles * 13312 / (bms / 1e3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
                 **at_held_clock(btiles * 13312 / (bms / 1e3) / 1e12, FP64_VALU_PEAK_TOPS,
-                                ["jpeg:void jpeg_strip_kernel<false, 2>",
-                                 "jpeg:void jpeg_strip_kernel<false>"]),
+                                ["jpeg:void jpeg_strip_kernel<false>"]),
                 "hbm_frac": round(8 * px * NB / (bms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
             "note": "images 0..127 of the continuous rand() stream: config 5's per-GPU share "
                     "at 8 GPUs, on one GPU",

@@ -189,11 +189,12 @@ int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
 /* Synchronise `stream` and report whether the last compress call on ctx met
  * a corrupt bucket head in lz4_tiles' LDS index (a head that is neither empty
  * nor an earlier position of the block: never on a sound LDS; the walk ends
- * anyway, chains strictly decrease): LZ4R_ERR_CORRUPT or LZ4R_OK.  It reads
- * LZ4R_LEN_CORRUPT of that call's length word; every call folds the kernel's
- * status into its own length word and clears it, so an async caller that
- * reads the length needs no separate check.  lz4r_compress_device checks by
- * itself. */
+ * anyway, chains strictly decrease): LZ4R_ERR_CORRUPT or LZ4R_OK.  It reads a
+ * verdict word the context owns, written by the call's last scan kernel
+ * beside LZ4R_LEN_CORRUPT of the call's length word (so the caller's length
+ * buffer may already be freed).  Every call folds the kernel's status into
+ * its own length word and clears it, so an async caller that reads the
+ * length needs no separate check.  lz4r_compress_device checks by itself. */
 int lz4r_check(lz4r_ctx *ctx, void *stream);
 
 /* Measurement: when enabled, every compress call records HIP events on its

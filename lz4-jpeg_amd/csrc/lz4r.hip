@@ -869,13 +869,17 @@ __global__ __launch_bounds__(64) void lz4_tiles(
 
   uint32_t *const recs = reinterpret_cast<uint32_t *>(slots + (size_t)t * kSlot);
   int W;
-  if (kAligned && t + 1 < nb) {
-    // every block but the launch's last: no staging, the keys come straight
-    // from global memory (encode_block<kFull>)
+  if (kAligned && (t + 2 < nb || (t + 2 == nb && last_n >= 24))) {
+    // no staging, the keys come straight from global memory
+    // (encode_block<kFull>): row 4's lanes read 24 bytes past the block end
+    // (and a mid-walk lcp drain up to 15), so only where those bytes are the
+    // launch's own -- every block but the last, and the one before it when
+    // the last holds at least 24 bytes
     W = encode_block<false, true>(S, kBlk, src, nullptr, recs, status);
   } else {
-    // the last block (n <= 300: nothing may be read past the input) or an
-    // unaligned input: staged bytewise, 16-B zero pad
+    // the last block (n <= 300: nothing may be read past the input), the one
+    // before a last block of < 24 bytes, or an unaligned input: staged
+    // bytewise, 16-B zero pad
     for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
     if (lane < 16) S.buf[kInOff + n + lane] = 0;
     wave_sync();
@@ -1456,13 +1460,16 @@ __global__ __launch_bounds__(256) void lz4_scan_reduce(const uint32_t *__restric
 // and leaves its end in *len.  The call's last scan (last != 0) also folds
 // lz4_tiles' corrupt-index status word into bit 63 of *len (kLenCorrupt) and
 // clears the word: every async caller gets the verdict in the length it
-// reads anyway, and the next call starts clean.
+// reads anyway, and the next call starts clean.  The same verdict goes to
+// *verdict, a word the context owns (lz4r_check reads it: the caller's
+// length buffer may be gone by then).
 constexpr uint64_t kLenCorrupt = 1ull << 63;
 __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__ part,
                                                           size_t nparts, uint64_t hdr,
                                                           int first, int last,
                                                           uint32_t *__restrict__ status,
-                                                          uint64_t *__restrict__ len) {
+                                                          uint64_t *__restrict__ len,
+                                                          uint64_t *__restrict__ verdict) {
   __shared__ uint64_t ws[16];
   __shared__ uint64_t carry;
   if (threadIdx.x == 0) carry = first ? hdr : *len;
@@ -1487,7 +1494,11 @@ __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__
   }
   if (threadIdx.x == 0) {
     uint64_t v = carry;
-    if (last && atomicExch(status, 0u) != 0u) v |= kLenCorrupt;
+    if (last) {
+      const bool bad = atomicExch(status, 0u) != 0u;
+      if (bad) v |= kLenCorrupt;
+      *verdict = bad ? 1u : 0u;
+    }
     *len = v;
   }
 }
@@ -1785,10 +1796,11 @@ struct lz4r_ctx {
   uint32_t *tsz = nullptr;     // encoded bytes per block (u32, for the scan)
   uint32_t *gsum = nullptr;    // encoded bytes per group of kGT blocks
   uint64_t *part = nullptr;    // scan partials, one per kPart blocks
-  uint64_t *len = nullptr;     // default device length slot, then the status word
+  uint64_t *len = nullptr;     // default device length slot, the status word, the verdict
   uint32_t *status = nullptr;  // (len + 1) nonzero once a block saw a corrupt bucket head
+  uint64_t *verdict = nullptr; // (len + 2) the last call's corrupt-index verdict (0 / 1)
   size_t last_nb = 0;
-  uint64_t *last_len = nullptr;  // the last call's length slot (its bit 63: corrupt index)
+  bool checkable = false;      // a call has launched (lz4r_check has a verdict to read)
   // timing: the call's start/end, and lz4_tiles' start/end in every chunk
   hipEvent_t ev_a = nullptr, ev_c = nullptr;
   std::vector<hipEvent_t> ev_tiles;   // 2 per chunk
@@ -1883,7 +1895,9 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
       // pairs of full blocks (lz4_pairs: two blocks per wave), then the last
       // one or two blocks of the chunk, one per wave (lz4_tiles); a pair's
       // second block is never the chunk's last (its 4-grams read 24 bytes on)
-      const size_t npairs = kPairs ? (nbc - 1) / 2 : 0;
+      // (B's row 4 reads 24 bytes into the block after it: with a last block
+      // of < 24 bytes the pair before it stays with lz4_tiles)
+      const size_t npairs = kPairs && nbc >= 2 ? (last_n >= 24 ? nbc - 1 : nbc - 2) / 2 : 0;
 #if LZ4R_PAIRS
       if (npairs) {
         const uint32_t pper = (uint32_t)((npairs + 7) / 8);
@@ -1907,7 +1921,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
                        c->gsum, c->part);
     hipLaunchKernelGGL(lz4_scan_partials, dim3(1), dim3(1024), 0, s, c->part + p0, np,
                        (uint64_t)hdr, k == 0 ? 1 : 0, k + 1 == nchunks ? 1 : 0, c->status,
-                       static_cast<uint64_t *>(d_len));
+                       static_cast<uint64_t *>(d_len), c->verdict);
     const size_t g0 = b0 / kGT, ng = (nbc + kGT - 1) / kGT;
     hipLaunchKernelGGL(lz4_emit, dim3((unsigned)(ng * kGSplit)), dim3(64 * kEW), 0, s, in, c->slots,
                        b0, c->tsz, b1, g0, c->gsum, c->part, static_cast<uint8_t *>(d_out),
@@ -1916,7 +1930,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   }
   if (timed) (void)hipEventRecord(c->ev_c, s);
   c->last_nb = nb;
-  c->last_len = static_cast<uint64_t *>(d_len);
+  c->checkable = true;
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess && getenv("LZ4R_DEBUG"))
     fprintf(stderr, "lz4r: %s\n", hipGetErrorString(e));
@@ -1946,13 +1960,14 @@ int lz4r_ctx_create(lz4r_ctx **out) {
   lz4r_ctx *c = new (std::nothrow) lz4r_ctx();
   if (!c) return LZ4R_ERR_NOMEM;
   if (hipGetDevice(&c->device) != hipSuccess ||
-      hipMalloc(&c->len, 2 * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(c->len, 0, 2 * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&c->len, 3 * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->len, 0, 3 * sizeof(uint64_t)) != hipSuccess ||
       hipEventCreate(&c->ev_a) != hipSuccess || hipEventCreate(&c->ev_c) != hipSuccess) {
     lz4r_ctx_destroy(c);
     return LZ4R_ERR_HIP;
   }
   c->status = reinterpret_cast<uint32_t *>(c->len + 1);
+  c->verdict = c->len + 2;
   *out = c;
   return LZ4R_OK;
 }
@@ -1984,7 +1999,7 @@ int lz4r_compress_segment_async(lz4r_ctx *c, const void *d_in, size_t n, void *d
   if (!final_shard && n % kBlk != 0) return LZ4R_ERR_ARG;
   if (n == 0) {                      // an empty shard (more ranks than blocks)
     c->last_nb = 0;
-    c->last_len = nullptr;
+    c->checkable = false;     // nothing launched: lz4r_check reports OK
     c->timed_call = false;
     return hipMemsetAsync(d_len, 0, sizeof(uint64_t), static_cast<hipStream_t>(stream)) ==
                    hipSuccess
@@ -2099,13 +2114,13 @@ int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t 
 
 int lz4r_check(lz4r_ctx *c, void *stream) {
   if (!c) return LZ4R_ERR_ARG;
-  if (!c->last_len) return LZ4R_OK;      // no launch yet (or an empty segment)
-  uint64_t v = 0;
+  if (!c->checkable) return LZ4R_OK;     // no launch yet (or an empty segment)
+  uint64_t v = 0;                        // the context's own verdict word
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipMemcpyAsync(&v, c->last_len, sizeof(v), hipMemcpyDeviceToHost, s) != hipSuccess ||
+  if (hipMemcpyAsync(&v, c->verdict, sizeof(v), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return LZ4R_ERR_HIP;
-  return (v & kLenCorrupt) ? LZ4R_ERR_CORRUPT : LZ4R_OK;
+  return v ? LZ4R_ERR_CORRUPT : LZ4R_OK;
 }
 
 int lz4r_set_timing(lz4r_ctx *c, int enable) {

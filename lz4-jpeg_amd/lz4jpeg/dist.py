@@ -114,7 +114,11 @@ def hip_segment_compressor(compressor, final_shard, stream=None):
                                   final_shard=final_shard)
         if stream is not None:
             stream.synchronize()      # .item() below waits only for torch's current stream
-        # raises on a corrupt LDS index (bit 63 of the length): the segment
-        # never reaches the gather
-        return out, compressor.async_length(d_len)
+        # the raw signed length: negative when the call flagged a corrupt LDS
+        # index (bit 63).  It is NOT raised here -- a rank that raised before
+        # the collective would leave the healthy ranks waiting in
+        # all_gather_into_tensor forever; exchange_lengths runs the gather
+        # first and then raises on every rank, so no segment reaches the
+        # gatherv
+        return out, int(d_len.item())
     return run

@@ -40,6 +40,28 @@ def test_no_self_launch_under_a_launcher_or_for_one_gpu():
     assert bench.maybe_self_launch(A, [], env={}) is None
 
 
+def test_dist_rehearsal_self_launches_one_rank():
+    """--dist at one GPU: the N > 1 code path as one launcher rank (the RCCL
+    rehearsal tests/test_gpu_rccl.py runs on the box); sharded workloads."""
+    class A:
+        gpus = 1
+        dist = True
+        lz4_bytes_per_rank = 1 << 30
+        jpeg_images_per_rank = 1
+        lz4_total_bytes = 0
+        jpeg_total_images = 0
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--dist",
+                        "--launch-check"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and lines[0]["world"] == 1 and lines[0]["scaling"] == "strong"
+    assert lines[0]["lz4_shard"] == [0, 64 << 30]
+    assert bench.workloads(1, A) == (64 << 30, 1024, "strong")
+
+
 def test_launcher_command_is_one_node_loopback():
     cmd = bench.launcher_cmd(4, ["--gpus", "4", "--steps", "3"], 29555)
     assert cmd[1:3] == ["-m", "torch.distributed.run"]

@@ -70,6 +70,51 @@ def test_sharded_stream_equals_single(oracle, world, n):
     assert q.get(timeout=5) is True
 
 
+def _corrupt_worker(rank, world, port, bad_rank, q):
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "lz4-jpeg_amd"))
+    from lz4jpeg import dist as d
+    from lz4jpeg.lz4 import Lz4Error
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        def seg(t):
+            # what hip_segment_compressor returns: the raw signed length, bit 63
+            # set (negative as int64) on the rank whose call flagged a corrupt
+            # LDS index
+            n = 1000 + rank
+            return torch.zeros(n, dtype=torch.uint8), (n | (1 << 63)) - (1 << 64) \
+                if rank == bad_rank else n
+
+        try:
+            d.compress_sharded(torch.zeros(600, dtype=torch.uint8), 600 * world, seg, dst=0)
+            q.put((rank, "no error"))
+        except Lz4Error as e:
+            q.put((rank, e.code))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad_rank", [0, 1])
+def test_corrupt_segment_raises_on_every_rank(bad_rank):
+    """One rank's segment carries LZ4R_LEN_CORRUPT: every rank raises
+    Lz4Error(-6) after the length all_gather -- none hangs in the collective,
+    none reaches the gatherv (a rank raising before the
+    all_gather deadlocked the others)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_corrupt_worker, args=(r, world, port, bad_rank, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0, "a rank hung or crashed"
+    got = dict(q.get(timeout=5) for _ in range(world))
+    assert got == {0: -6, 1: -6}
+
+
 def test_shards_are_block_aligned_and_cover():
     for n in [300, 301, 12345, 10 ** 6 + 7, 1 << 30]:
         for world in [1, 2, 3, 4, 8]:

@@ -83,8 +83,9 @@ def test_batch_equals_singles(gpu, oracle):
 
 
 def test_batch_odd_strip_count(gpu, oracle):
-    # a multi-image launch runs two strips per workgroup: 3 strips per image
-    # (one 25-tile strip per tile row) leaves each image's last workgroup one
+    # a batched launch whose images each end in a ragged strip: a 200x24
+    # image is 3 tile rows of 25 tiles, i.e. one short strip (25 of 32 tiles)
+    # per row, and the strips of image k + 1 follow image k's in one grid
     from lz4jpeg import synth
     imgs = np.stack([synth.rand_rgba(200, 24, seed=s) for s in (7, 8, 9)])
     got = _enc(imgs, nimg=3).reshape(3, -1)

@@ -94,6 +94,60 @@ def test_fuzz_vs_oracle(comp, oracle, idx):
     assert _gpu_compress(comp, data) == oracle.lz4_compress(data)
 
 
+@pytest.mark.parametrize("n", [301, 308, 300 * 2 + 4, 300 * 77 + 20, 300 * 5 + 24])
+def test_input_ending_at_allocation_end(comp, oracle, n):
+    """A last block of 1..23 bytes: the block before it must not read its
+    24 bytes past its own end (the unstaged 4-gram loads) beyond the input.
+    The input sits at the very end of its own hipMalloc allocation (raw, not
+    torch's caching allocator), 4-byte aligned when n is (the unstaged path);
+    with the over-read those loads would leave the allocation."""
+    import ctypes
+    import torch
+    from lz4jpeg import _lib
+    from lz4jpeg.lz4 import compress_bound
+    torch.cuda.init()
+    hip = ctypes.CDLL("libamdhip64.so")
+    text = golden_inputs.lz4_input("metamorphosis_spaces")
+    data = bytes(text[1000:1000 + n])
+    size = 64 << 10                                 # a page multiple
+    p = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(size)) == 0
+    try:
+        src = ctypes.c_void_p(p.value + size - n)   # the input ends at the allocation end
+        assert hip.hipMemcpy(src, data, ctypes.c_size_t(n), 1) == 0   # host -> device
+        d_out = torch.empty(compress_bound(n), dtype=torch.uint8, device="cuda")
+        got = ctypes.c_size_t(0)
+        torch.cuda.synchronize()
+        rc = _lib.lib().lz4r_compress_device(comp._h, src, n, ctypes.c_void_p(d_out.data_ptr()),
+                                             d_out.numel(), ctypes.byref(got), None)
+        assert rc == 0
+        assert d_out[:got.value].cpu().numpy().tobytes() == oracle.lz4_compress(data)
+    finally:
+        hip.hipFree(p)
+
+
+def test_check_reads_the_contexts_own_verdict(comp):
+    """lz4r_check after an async call whose length buffer is already freed:
+    it reads a word the context owns, not the caller's buffer,
+    and an empty segment (no launch) reports OK."""
+    import torch
+    from lz4jpeg.lz4 import compress_bound
+    data = golden_inputs.lz4_input("text_10000")
+    d_in = torch.from_numpy(np.frombuffer(bytes(data), dtype=np.uint8).copy()).cuda()
+    d_out = torch.empty(compress_bound(len(data)), dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(1, dtype=torch.int64, device="cuda")
+    comp.compress_async(d_in, len(data), d_out, d_len)
+    del d_len
+    torch.cuda.empty_cache()
+    junk = torch.full((1 << 20,), -1, dtype=torch.int64, device="cuda")   # reuse the memory
+    comp.check()
+    del junk
+    d_len = torch.zeros(1, dtype=torch.int64, device="cuda")
+    comp.compress_async(d_in, 0, d_out, d_len, segment=True, final_shard=True)
+    comp.check()
+    assert comp.async_length(d_len) == 0
+
+
 def test_segments_concatenate_to_stream(comp, oracle):
     """Shard outputs (lz4r_compress_segment_async) + header byte == framed stream."""
     import torch
