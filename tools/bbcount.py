@@ -1,0 +1,305 @@
+"""Per-basic-block dynamic instruction counts of lz4_tiles (tools only).
+
+The roof of an issue-bound kernel needs the dynamic count of every opcode, not
+only the SQ_INSTS_* totals, because gfx950 VALU opcodes do not cost the same
+(profiles/r03_valu_rate.log: v_add/and/or/xor ~2.3 cycles per wave-instruction
+per SIMD, VOP3-only / SGPR-operand / DPP / VOPC ~4, 64-bit shifts ~5.6).
+
+  build   compile csrc/lz4r.hip with the product's HIPFLAGS to assembly, insert
+          after every basic-block label of lz4_tiles<true> (and the inline-asm
+          walk loop's local label) a counter bump -- EXEC saved to s[80:81],
+          EXEC = lane 0, one vector global_atomic_add of 1 into
+          lz4r_bb_acc[bb], EXEC restored -- so a block entered with EXEC = 0
+          still counts (its VALU instructions still issue), assemble the code
+          object (tools/ab/bbcnt.co) and write the static opcode list of every
+          basic block of the UNinstrumented code (tools/ab/bb_static.json).
+          The compiled kernel uses v0..v46 and s0..s31, so v60..v62 and
+          s[80:81] are free; the descriptor is raised to cover them.
+  run     (GPU box) load the code object as a module, compress the bench
+          corpus (1 GiB, synthesised on the device) with it once, read the
+          counters -> <out>/bbcounts.json.
+  report  counts x static opcode lists -> dynamic opcodes per 300-B block,
+          the cost-weighted VALU cycles (tools/valu_cost.py classes) and the
+          per-pipe roof, optionally against a PMC summary.
+"""
+import collections
+import ctypes
+import json
+import os
+import re
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(REPO, "tools", "ab")
+LLVM = "/opt/rocm/lib/llvm/bin"
+KERNEL = "_ZN12_GLOBAL__N_19lz4_tilesILb1EEEvPKhjjjPhPjPtS4_"
+NCNT = 1024
+LABEL = re.compile(r"^(\.LBB\d+_\d+):|^; (%bb\.\d+):|^\s*(1):\s*$")
+
+
+def hipflags():
+    out = subprocess.run(["make", "-s", "-C", REPO, "print-HIPFLAGS"], check=True,
+                         capture_output=True, text=True).stdout.split()
+    return [f for f in out if f not in ("-fPIC",)]
+
+
+def compile_asm(src, extra=()):
+    os.makedirs(OUT, exist_ok=True)
+    s = os.path.join(OUT, "bb_src.s")
+    subprocess.run(["/opt/rocm/bin/hipcc", *hipflags(), *extra, "--cuda-device-only", "-S", src,
+                    "-o", s], check=True, stderr=subprocess.DEVNULL)
+    return open(s).read().splitlines()
+
+
+def kernel_range(L, name=KERNEL):
+    st = next(i for i, l in enumerate(L) if l.startswith(name + ":"))
+    en = next(i for i in range(st, len(L)) if L[i].startswith(".Lfunc_end"))
+    return st, en
+
+
+def opcode(line):
+    """The instruction text (opcode and operands) of an assembly line, or None."""
+    t = line.split(";")[0].strip()
+    if not t or t.startswith(".") or t.endswith(":") or t.startswith("//"):
+        return None
+    return " ".join(t.split())
+
+
+def basic_blocks(L, st, en):
+    """[(label, [opcodes])] of the function body: the entry block, then one
+    per label (LLVM labels, fallthrough %bb comments, the asm loop's 1:)."""
+    bbs = [("entry", [])]
+    for i in range(st + 1, en):
+        m = LABEL.match(L[i])
+        if m:
+            bbs.append((next(g for g in m.groups() if g), []))
+            continue
+        op = opcode(L[i])
+        if op:
+            bbs[-1][1].append(op)
+    return bbs
+
+
+BUMP = ["\ts_mov_b64 s[80:81], exec",
+        "\ts_mov_b64 exec, 1",
+        "\ts_nop 1",
+        "\tglobal_atomic_add v[60:61], v62, off offset:{off}",
+        "\ts_mov_b64 exec, s[80:81]",
+        "\ts_nop 1"]
+PROLOGUE = ["\ts_getpc_b64 s[80:81]",
+            "\ts_add_u32 s80, s80, lz4r_bb_acc@rel32@lo+4",
+            "\ts_addc_u32 s81, s81, lz4r_bb_acc@rel32@hi+12",
+            "\tv_mov_b32 v60, s80",
+            "\tv_mov_b32 v61, s81",
+            "\tv_mov_b32 v62, 1"]
+
+
+def instrument(L, st, en):
+    body = L[st:en]
+    used = set()
+    for l in body:
+        t = l.split(";")[0]
+        for r in re.findall(r"\bv\[?(\d+)", t):
+            used.add(("v", int(r)))
+        for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", t):
+            used.update(("v", k) for k in range(int(a), int(b) + 1))
+        for a, b in re.findall(r"\bs\[(\d+):(\d+)\]", t):
+            used.update(("s", k) for k in range(int(a), int(b) + 1))
+        for r in re.findall(r"\bs(\d+)\b", t):
+            used.add(("s", int(r)))
+    assert max(k for t, k in used if t == "v") < 60, "v60.. in use"
+    assert max(k for t, k in used if t == "s") < 80, "s80.. in use"
+    out = list(L[:st + 1]) + PROLOGUE
+    k = 0
+    off = lambda k: f"{4 * k}"
+    out += [b.format(off=off(k)) for b in BUMP]      # entry block
+    k += 1
+    for i in range(st + 1, en):
+        out.append(L[i])
+        if LABEL.match(L[i]):
+            out += [b.format(off=off(k)) for b in BUMP]
+            k += 1
+    assert k <= NCNT and 4 * k < 4096
+    out += L[en:]
+    txt = "\n".join(out)
+    # descriptor / metadata: cover v60..v62 and s80..s81
+    txt = re.sub(r"(\.amdhsa_kernel " + KERNEL + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_vgpr )\d+",
+                 r"\g<1>64", txt)
+    txt = re.sub(r"(\.amdhsa_kernel " + KERNEL + r"\n(?:.*\n)*?\s*\.amdhsa_accum_offset )\d+",
+                 r"\g<1>64", txt)
+    txt = re.sub(r"(\.amdhsa_kernel " + KERNEL + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_sgpr )\d+",
+                 r"\g<1>84", txt)
+    txt += ("\n\t.type\tlz4r_bb_acc,@object\n\t.section\t.bss.lz4r_bb_acc,\"aw\",@nobits\n"
+            "\t.globl\tlz4r_bb_acc\n\t.protected\tlz4r_bb_acc\n\t.p2align\t8\nlz4r_bb_acc:\n\t.zero\t4096\n"
+            "\t.size\tlz4r_bb_acc, 4096\n")
+    return txt, k
+
+
+def build():
+    L = compile_asm(os.path.join(REPO, "lz4-jpeg_amd", "csrc", "lz4r.hip"))
+    st, en = kernel_range(L)
+    bbs = basic_blocks(L, st, en)
+    txt, k = instrument(L, st, en)
+    assert k == len(bbs), (k, len(bbs))
+    s = os.path.join(OUT, "bbcnt.s")
+    open(s, "w").write(txt)
+    o = os.path.join(OUT, "bbcnt.o")
+    subprocess.run([f"{LLVM}/clang", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c", s,
+                    "-o", o], check=True)
+    subprocess.run([f"{LLVM}/ld.lld", "-shared", o, "-o", os.path.join(OUT, "bbcnt.co")],
+                   check=True)
+    json.dump({"kernel": KERNEL, "bbs": bbs}, open(os.path.join(OUT, "bb_static.json"), "w"))
+    print(f"{len(bbs)} basic blocks, {sum(len(b) for _, b in bbs)} static instructions")
+
+
+def run(outdir, nbytes=1 << 30):
+    sys.path.insert(0, os.path.join(REPO, "lz4-jpeg_amd"))
+    import torch
+    from lz4jpeg import synth
+    hip = ctypes.CDLL("libamdhip64.so")
+    torch.cuda.init()
+    dev = torch.device("cuda", 0)
+    n = nbytes
+    d_in = torch.empty(n + 16, dtype=torch.uint8, device=dev)
+    synth.random_passages_device(d_in, n, length=30000, seed=1, first=0)
+    nb = (n + 299) // 300
+    assert nb <= 1 << 24
+    last_n = n - (nb - 1) * 300
+    slots = torch.empty(nb * 640, dtype=torch.uint8, device=dev)
+    usz = torch.empty(nb, dtype=torch.int32, device=dev)
+    bsz = torch.empty(nb, dtype=torch.int16, device=dev)
+    status = torch.zeros(2, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    mod = ctypes.c_void_p()
+    assert hip.hipModuleLoad(ctypes.byref(mod), os.path.join(OUT, "bbcnt.co").encode()) == 0
+    fn = ctypes.c_void_p()
+    assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, KERNEL.encode()) == 0
+    acc, accsz = ctypes.c_void_p(), ctypes.c_size_t()
+    assert hip.hipModuleGetGlobal(ctypes.byref(acc), ctypes.byref(accsz), mod,
+                                  b"lz4r_bb_acc") == 0
+    assert hip.hipMemset(acc, 0, ctypes.c_size_t(4 * NCNT)) == 0
+    per = (nb + 7) // 8
+    args = [ctypes.c_void_p(d_in.data_ptr()), ctypes.c_uint32(nb), ctypes.c_uint32(per),
+            ctypes.c_uint32(last_n), ctypes.c_void_p(slots.data_ptr()),
+            ctypes.c_void_p(usz.data_ptr()), ctypes.c_void_p(bsz.data_ptr()),
+            ctypes.c_void_p(status.data_ptr())]
+    params = (ctypes.c_void_p * len(args))(*[ctypes.cast(ctypes.pointer(a), ctypes.c_void_p)
+                                              for a in args])
+    assert hip.hipModuleLaunchKernel(fn, 8 * per, 1, 1, 64, 1, 1, 0, None, params, None) == 0
+    assert hip.hipDeviceSynchronize() == 0
+    host = (ctypes.c_uint32 * NCNT)()
+    assert hip.hipMemcpy(host, acc, ctypes.c_size_t(4 * NCNT), 2) == 0
+    # the encoded sizes must equal the product's (the instrumentation changes no result)
+    import numpy as np
+    from lz4jpeg import lz4
+    comp = lz4.Compressor()
+    _, got = comp.compress_device(d_in, n)
+    off = comp.block_offsets(nb).astype(np.int64)
+    prod = np.diff(np.append(off, got - 1))
+    same = bool((prod == usz.cpu().numpy().astype(np.int64)).all())
+    os.makedirs(outdir, exist_ok=True)
+    res = {"bytes": n, "blocks": nb, "status": int(status[0].item()),
+           "sizes_equal_product": same, "counts": list(host)}
+    json.dump(res, open(os.path.join(outdir, "bbcounts.json"), "w"))
+    print(json.dumps({k: v for k, v in res.items() if k != "counts"}))
+
+
+# cycles per wave-instruction per SIMD at 8 waves per SIMD (tools/valu_rate.hip;
+# profiles/r03_valu_rate.log, profiles/r05_valu_rate.log)
+FAST = {"v_add_u32", "v_xor_b32", "v_and_b32", "v_or_b32"}
+
+
+def vcost(ins, table):
+    op = ins.split()[0]
+    base = re.sub(r"_e(32|64)$", "", op)
+    args = ins.split(None, 1)[1] if " " in ins else ""
+    srcs = ",".join(args.split(",")[1:])
+    sgpr_src = bool(re.search(r"\bs\[?\d", srcs)) or "exec" in srcs
+    if "_dpp" in op or " row_" in ins or "wave_sh" in ins or "quad_perm" in ins:
+        return table["dpp"]
+    if base in FAST:
+        return table["vop2_sgpr"] if sgpr_src else table["fast"]
+    for k in ("v_lshlrev_b64", "v_lshrrev_b64", "v_ashrrev_i64"):
+        if base == k:
+            return table["shift64"]
+    if base in table:
+        return table[base]
+    if base == "v_cndmask_b32" and op.endswith("_e32"):
+        return table["v_cndmask_b32_e32_vcc_valu"]
+    return table["default"]
+
+
+def classify(ins):
+    op = ins.split()[0]
+    if op.startswith("v_"):
+        return "valu"
+    if op.startswith("ds_"):
+        return "lds"
+    if op.startswith(("global_", "buffer_", "flat_", "scratch_")):
+        return "vmem"
+    if op.startswith(("s_load", "s_buffer_load")):
+        return "smem"
+    if op.startswith(("s_cbranch", "s_branch")):
+        return "branch"
+    if op in ("s_waitcnt", "s_nop", "s_endpgm", "s_barrier", "s_setprio", "s_sleep"):
+        return op
+    if op.startswith("s_"):
+        return "salu"
+    return "other"
+
+
+def report(countsf, staticf, costf=None, pmcf=None, clock_ghz=None, ms_per_gib=None):
+    C = json.load(open(countsf))
+    S = json.load(open(staticf))
+    nbk = C["blocks"]
+    counts = C["counts"]
+    bbs = S["bbs"]
+    assert len(counts) >= len(bbs)
+    dyn = collections.Counter()
+    per_bb = []
+    for (lab, ins), c in zip(bbs, counts):
+        for x in ins:
+            dyn[x] += c
+        per_bb.append((lab, c / nbk, ins))
+    cls = collections.Counter()
+    ops = collections.Counter()
+    for x, c in dyn.items():
+        cls[classify(x)] += c / nbk
+        ops[x.split()[0]] += c / nbk
+    table = json.load(open(costf)) if costf else None
+    out = {"blocks": nbk, "per_block": {k: round(v, 2) for k, v in sorted(cls.items())},
+           "opcodes_per_block": {k: round(v, 2) for k, v in ops.most_common()}}
+    if table:
+        vcyc = sum(vcost(x, table) * c for x, c in dyn.items() if classify(x) == "valu") / nbk
+        scyc = table["salu"] * cls["salu"]
+        out["valu_cycles_per_block_per_simd"] = round(vcyc, 1)
+        out["salu_cycles_per_block_per_simd"] = round(scyc, 1)
+        bycost = collections.Counter()
+        for x, c in dyn.items():
+            if classify(x) == "valu":
+                bycost[x.split()[0]] += vcost(x, table) * c / nbk
+        out["valu_cycles_by_opcode"] = {k: round(v, 1) for k, v in bycost.most_common(40)}
+        hot = []
+        for lab, c, ins in per_bb:
+            v = sum(vcost(x, table) for x in ins if classify(x) == "valu") * c
+            sa = sum(1 for x in ins if classify(x) == "salu") * c * table["salu"]
+            hot.append((v, lab, round(c, 3), len(ins), round(sa, 1)))
+        hot.sort(reverse=True)
+        out["hot_blocks"] = [{"bb": l, "execs_per_block": c, "static": n,
+                              "valu_cycles": round(v, 1), "salu_cycles": sa}
+                             for v, l, c, n, sa in hot[:40]]
+    print(json.dumps(out, indent=1))
+    return out
+
+
+if __name__ == "__main__":
+    cmd = sys.argv[1]
+    if cmd == "build":
+        build()
+    elif cmd == "report":
+        report(*sys.argv[2:5])
+    elif cmd == "run":
+        run(sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out", "bbcount"))
+    else:
+        raise SystemExit(__doc__)

@@ -186,6 +186,91 @@ __global__ __launch_bounds__(64) void body(uint32_t *out, uint64_t *clk) {
           : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=s"(t0), "=s"(t1));
       s0 ^= t0;
       s1 ^= t1;
+    } else if (KIND == 23) { // 8 v_mov_b32_e32 (VOP1 copy)
+      asm volatile(
+          "v_mov_b32_e32 %0, %1\n\tv_mov_b32_e32 %1, %2\n\tv_mov_b32_e32 %2, %3\n\t"
+          "v_mov_b32_e32 %3, %0\n\tv_mov_b32_e32 %0, %2\n\tv_mov_b32_e32 %1, %3\n\t"
+          "v_mov_b32_e32 %2, %0\n\tv_mov_b32_e32 %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 24) { // 8 v_sub_u32_e32
+      asm volatile(
+          "v_sub_u32_e32 %0, %0, %1\n\tv_sub_u32_e32 %1, %1, %2\n\tv_sub_u32_e32 %2, %2, %3\n\t"
+          "v_sub_u32_e32 %3, %3, %0\n\tv_sub_u32_e32 %0, %0, %2\n\tv_sub_u32_e32 %1, %1, %3\n\t"
+          "v_sub_u32_e32 %2, %2, %0\n\tv_sub_u32_e32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 25) { // 8 v_lshlrev_b32_e32 / v_lshrrev_b32_e32 (VGPR shift)
+      asm volatile(
+          "v_lshlrev_b32_e32 %0, %1, %0\n\tv_lshrrev_b32_e32 %1, %2, %1\n\t"
+          "v_lshlrev_b32_e32 %2, %3, %2\n\tv_lshrrev_b32_e32 %3, %0, %3\n\t"
+          "v_lshlrev_b32_e32 %0, 3, %0\n\tv_lshrrev_b32_e32 %1, 2, %1\n\t"
+          "v_lshlrev_b32_e32 %2, 5, %2\n\tv_lshrrev_b32_e32 %3, 7, %3\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 26) { // 8 v_max_u32_e32 / v_min_u32_e32
+      asm volatile(
+          "v_max_u32_e32 %0, %0, %1\n\tv_min_u32_e32 %1, %1, %2\n\tv_max_u32_e32 %2, %2, %3\n\t"
+          "v_min_u32_e32 %3, %3, %0\n\tv_max_u32_e32 %0, %0, %2\n\tv_min_u32_e32 %1, %1, %3\n\t"
+          "v_max_u32_e32 %2, %2, %0\n\tv_min_u32_e32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 27) { // 8 v_lshl_add_u64 (64-bit address arithmetic)
+      uint64_t x = ((uint64_t)a << 32) | b, y = ((uint64_t)c << 32) | d;
+      asm volatile(
+          "v_lshl_add_u64 %0, %0, 2, %1\n\tv_lshl_add_u64 %1, %1, 1, %0\n\t"
+          "v_lshl_add_u64 %0, %0, 0, %1\n\tv_lshl_add_u64 %1, %1, 3, %0\n\t"
+          "v_lshl_add_u64 %0, %0, 2, %1\n\tv_lshl_add_u64 %1, %1, 1, %0\n\t"
+          "v_lshl_add_u64 %0, %0, 0, %1\n\tv_lshl_add_u64 %1, %1, 3, %0\n\t"
+          : "+v"(x), "+v"(y));
+      a = (uint32_t)x; b = (uint32_t)(x >> 32); c = (uint32_t)y; d = (uint32_t)(y >> 32);
+    } else if (KIND == 28) { // 8 s_nop 0
+      asm volatile("s_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0");
+    } else if (KIND == 29) { // 8 v_bfi_b32 / v_xad_u32 / v_min3_u32 / v_max3_i32
+      asm volatile(
+          "v_bfi_b32 %0, %1, %2, %3\n\tv_xad_u32 %1, %2, %3, %0\n\t"
+          "v_min3_u32 %2, %3, %0, %1\n\tv_max3_i32 %3, %0, %1, %2\n\t"
+          "v_bfi_b32 %0, %1, %2, %3\n\tv_xad_u32 %1, %2, %3, %0\n\t"
+          "v_min3_u32 %2, %3, %0, %1\n\tv_max3_i32 %3, %0, %1, %2\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 30) { // 8 v_cndmask_b32_e32 on a VCC written by VALU (v_cmp_e32)
+      asm volatile(
+          "v_cmp_lt_u32_e32 vcc, %0, %1\n\t"
+          "v_cndmask_b32_e32 %0, %0, %1, vcc\n\tv_cndmask_b32_e32 %1, %1, %2, vcc\n\t"
+          "v_cndmask_b32_e32 %2, %2, %3, vcc\n\tv_cndmask_b32_e32 %3, %3, %0, vcc\n\t"
+          "v_cndmask_b32_e32 %0, %0, %1, vcc\n\tv_cndmask_b32_e32 %1, %1, %2, vcc\n\t"
+          "v_cndmask_b32_e32 %2, %2, %3, vcc\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : : "vcc");
+    } else if (KIND == 31) { // 4 s_and_b64 mask -> v_cndmask_b32_e64 at once (SALU -> VALU lane mask)
+      uint64_t m = 0;
+      asm volatile(
+          "s_and_b64 %4, %5, %6\n\tv_cndmask_b32_e64 %0, %0, %1, %4\n\t"
+          "s_xor_b64 %4, %4, %6\n\tv_cndmask_b32_e64 %1, %1, %2, %4\n\t"
+          "s_and_b64 %4, %4, %5\n\tv_cndmask_b32_e64 %2, %2, %3, %4\n\t"
+          "s_or_b64 %4, %4, %6\n\tv_cndmask_b32_e64 %3, %3, %0, %4\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=&s"(m)
+          : "s"((uint64_t)s0 * 0x9E3779B97F4A7C15ull), "s"((uint64_t)s1 * 0xC2B2AE3D27D4EB4Full)
+          : "scc");
+      s0 ^= (uint32_t)m;
+    } else if (KIND == 32) { // 4 v_cmp_e64 -> s_and_saveexec-free: ballot then s_bcnt1 (VALU -> SALU)
+      uint64_t m = 0;
+      uint32_t cnt = 0;
+      asm volatile(
+          "v_cmp_lt_u32_e64 %4, %0, %1\n\ts_bcnt1_i32_b64 %5, %4\n\t"
+          "v_cmp_lt_u32_e64 %4, %2, %3\n\ts_bcnt1_i32_b64 %5, %4\n\t"
+          "v_cmp_lt_u32_e64 %4, %1, %2\n\ts_bcnt1_i32_b64 %5, %4\n\t"
+          "v_cmp_lt_u32_e64 %4, %3, %0\n\ts_bcnt1_i32_b64 %5, %4\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=&s"(m), "=&s"(cnt) : : "scc");
+      s0 ^= cnt;
+    } else if (KIND == 33) { // 8 v_writelane_b32 (SGPR lane select)
+      asm volatile(
+          "v_writelane_b32 %0, %4, 3\n\tv_writelane_b32 %1, %4, 7\n\t"
+          "v_writelane_b32 %2, %4, 11\n\tv_writelane_b32 %3, %4, 13\n\t"
+          "v_writelane_b32 %0, %4, 17\n\tv_writelane_b32 %1, %4, 19\n\t"
+          "v_writelane_b32 %2, %4, 23\n\tv_writelane_b32 %3, %4, 29\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "s"(s0));
+    } else if (KIND == 34) { // 8 v_ffbl_b32 alone
+      asm volatile(
+          "v_ffbl_b32_e32 %0, %1\n\tv_ffbl_b32_e32 %1, %2\n\tv_ffbl_b32_e32 %2, %3\n\t"
+          "v_ffbl_b32_e32 %3, %0\n\tv_ffbl_b32_e32 %0, %2\n\tv_ffbl_b32_e32 %1, %3\n\t"
+          "v_ffbl_b32_e32 %2, %0\n\tv_ffbl_b32_e32 %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
     } else {                 // 4 VALU + 4 SALU interleaved
       asm volatile(
           "v_add_u32 %0, %0, %1\n\ts_add_u32 %4, %4, %5\n\tv_add_u32 %1, %1, %2\n\t"
@@ -256,5 +341,17 @@ int main() {
   run<20>("VOP2 + sgpr", grid, out, clk);
   run<21>("v_add/xor_e64 (VOP3 enc)", grid, out, clk);
   run<22>("v_readfirstlane/readlane", grid, out, clk);
+  run<23>("v_mov_b32_e32", grid, out, clk);
+  run<24>("v_sub_u32_e32", grid, out, clk);
+  run<25>("v_lshl/lshrrev_b32_e32", grid, out, clk);
+  run<26>("v_max/min_u32_e32", grid, out, clk);
+  run<27>("v_lshl_add_u64", grid, out, clk);
+  run<28>("s_nop 0", grid, out, clk);
+  run<29>("v_bfi/xad/min3/max3", grid, out, clk);
+  run<30>("v_cndmask_e32 vcc<-valu", grid, out, clk);
+  run<31>("salu mask->v_cndmask (8)", grid, out, clk);
+  run<32>("v_cmp->s_bcnt1 (8)", grid, out, clk);
+  run<33>("v_writelane_b32", grid, out, clk);
+  run<34>("v_ffbl_b32_e32", grid, out, clk);
   return 0;
 }
