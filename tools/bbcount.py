@@ -136,24 +136,26 @@ def instrument(L, st, en):
     return txt, k
 
 
-def build():
-    L = compile_asm(os.path.join(REPO, "lz4-jpeg_amd", "csrc", "lz4r.hip"))
+def build(src=None, name="prod"):
+    src = src or os.path.join(REPO, "lz4-jpeg_amd", "csrc", "lz4r.hip")
+    L = compile_asm(src)
     st, en = kernel_range(L)
     bbs = basic_blocks(L, st, en)
     txt, k = instrument(L, st, en)
     assert k == len(bbs), (k, len(bbs))
-    s = os.path.join(OUT, "bbcnt.s")
+    s = os.path.join(OUT, f"bbcnt_{name}.s")
     open(s, "w").write(txt)
-    o = os.path.join(OUT, "bbcnt.o")
+    o = os.path.join(OUT, f"bbcnt_{name}.o")
     subprocess.run([f"{LLVM}/clang", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c", s,
                     "-o", o], check=True)
-    subprocess.run([f"{LLVM}/ld.lld", "-shared", o, "-o", os.path.join(OUT, "bbcnt.co")],
+    subprocess.run([f"{LLVM}/ld.lld", "-shared", o, "-o", os.path.join(OUT, f"bbcnt_{name}.co")],
                    check=True)
-    json.dump({"kernel": KERNEL, "bbs": bbs}, open(os.path.join(OUT, "bb_static.json"), "w"))
+    json.dump({"kernel": KERNEL, "bbs": bbs},
+              open(os.path.join(OUT, f"bb_static_{name}.json"), "w"))
     print(f"{len(bbs)} basic blocks, {sum(len(b) for _, b in bbs)} static instructions")
 
 
-def run(outdir, nbytes=1 << 30):
+def run(outdir, name="prod", nbytes=1 << 30):
     sys.path.insert(0, os.path.join(REPO, "lz4-jpeg_amd"))
     import torch
     from lz4jpeg import synth
@@ -172,7 +174,8 @@ def run(outdir, nbytes=1 << 30):
     status = torch.zeros(2, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     mod = ctypes.c_void_p()
-    assert hip.hipModuleLoad(ctypes.byref(mod), os.path.join(OUT, "bbcnt.co").encode()) == 0
+    assert hip.hipModuleLoad(ctypes.byref(mod),
+                             os.path.join(OUT, f"bbcnt_{name}.co").encode()) == 0
     fn = ctypes.c_void_p()
     assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, KERNEL.encode()) == 0
     acc, accsz = ctypes.c_void_p(), ctypes.c_size_t()
@@ -194,14 +197,14 @@ def run(outdir, nbytes=1 << 30):
     import numpy as np
     from lz4jpeg import lz4
     comp = lz4.Compressor()
-    _, got = comp.compress_device(d_in, n)
+    _, got = comp.compress_device(d_in, n)   # (the product library's result)
     off = comp.block_offsets(nb).astype(np.int64)
     prod = np.diff(np.append(off, got - 1))
     same = bool((prod == usz.cpu().numpy().astype(np.int64)).all())
     os.makedirs(outdir, exist_ok=True)
     res = {"bytes": n, "blocks": nb, "status": int(status[0].item()),
            "sizes_equal_product": same, "counts": list(host)}
-    json.dump(res, open(os.path.join(outdir, "bbcounts.json"), "w"))
+    json.dump(res, open(os.path.join(outdir, f"bbcounts_{name}.json"), "w"))
     print(json.dumps({k: v for k, v in res.items() if k != "counts"}))
 
 
@@ -295,11 +298,11 @@ def report(countsf, staticf, costf=None, pmcf=None, clock_ghz=None, ms_per_gib=N
 
 if __name__ == "__main__":
     cmd = sys.argv[1]
-    if cmd == "build":
-        build()
+    if cmd == "build":              # build [src.hip name]
+        build(*sys.argv[2:4])
     elif cmd == "report":
         report(*sys.argv[2:5])
     elif cmd == "run":
-        run(sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out", "bbcount"))
+        run(sys.argv[2], *sys.argv[3:4])   # run outdir [name]
     else:
         raise SystemExit(__doc__)

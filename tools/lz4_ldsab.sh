@@ -1,6 +1,6 @@
 # lz4_tiles PMC A/B: instruction mix, wave-cycle breakdown and LDS array
 # counters per block (per wave) for the product build and each variant
-# tools/variants/liblz4_<v>.so named as an argument.
+# tools/ab/liblz4_<v>.so named as an argument.
 # usage: bash tools/lz4_ldsab.sh v1 v2 ...  -> gpurun_out/ldsab/summary.txt
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -35,4 +35,4 @@ print(f"   lz4_tiles {ns / 1e3:.1f} us / 256 MiB; per block: " +
 PY
 }
 run product $PWD/lz4-jpeg_amd/lz4jpeg/liblz4jpeg.so || exit 1
-for v in "$@"; do run $v $PWD/tools/variants/liblz4_$v.so || exit 1; done
+for v in "$@"; do run $v $PWD/tools/ab/liblz4_$v.so || exit 1; done

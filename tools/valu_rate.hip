@@ -12,6 +12,8 @@ template <int KIND>
 __global__ __launch_bounds__(64) void body(uint32_t *out, uint64_t *clk) {
   uint32_t a = threadIdx.x, b = a * 3u, c = a * 5u, d = a * 7u;
   uint32_t s0 = blockIdx.x, s1 = s0 * 3u;
+  if (KIND == 35 || KIND == 36)
+    asm volatile("s_mov_b64 vcc, %0" : : "s"((uint64_t)s0 * 0x9E3779B97F4A7C15ull) : "vcc");
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
   for (int i = 0; i < REP; ++i) {
@@ -271,6 +273,63 @@ __global__ __launch_bounds__(64) void body(uint32_t *out, uint64_t *clk) {
           "v_ffbl_b32_e32 %3, %0\n\tv_ffbl_b32_e32 %0, %2\n\tv_ffbl_b32_e32 %1, %3\n\t"
           "v_ffbl_b32_e32 %2, %0\n\tv_ffbl_b32_e32 %3, %1\n\t"
           : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 35) { // 8 v_cndmask_b32_e32 on a VCC set once before the loop
+      asm volatile(
+          "v_cndmask_b32_e32 %0, %0, %1, vcc\n\tv_cndmask_b32_e32 %1, %1, %2, vcc\n\t"
+          "v_cndmask_b32_e32 %2, %2, %3, vcc\n\tv_cndmask_b32_e32 %3, %3, %0, vcc\n\t"
+          "v_cndmask_b32_e32 %0, %0, %1, vcc\n\tv_cndmask_b32_e32 %1, %1, %2, vcc\n\t"
+          "v_cndmask_b32_e32 %2, %2, %3, vcc\n\tv_cndmask_b32_e32 %3, %3, %0, vcc\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : : );
+    } else if (KIND == 36) { // 8 v_cndmask_b32_e64 reading vcc (set once before the loop)
+      asm volatile(
+          "v_cndmask_b32_e64 %0, %0, %1, vcc\n\tv_cndmask_b32_e64 %1, %1, %2, vcc\n\t"
+          "v_cndmask_b32_e64 %2, %2, %3, vcc\n\tv_cndmask_b32_e64 %3, %3, %0, vcc\n\t"
+          "v_cndmask_b32_e64 %0, %0, %1, vcc\n\tv_cndmask_b32_e64 %1, %1, %2, vcc\n\t"
+          "v_cndmask_b32_e64 %2, %2, %3, vcc\n\tv_cndmask_b32_e64 %3, %3, %0, vcc\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : : );
+    } else if (KIND == 37) { // 4 x (v_cmp_e64 -> SGPR pair, v_cndmask_b32_e64 on it at once)
+      uint64_t m = 0;
+      asm volatile(
+          "v_cmp_lt_u32_e64 %4, %0, %1\n\tv_cndmask_b32_e64 %1, %1, %2, %4\n\t"
+          "v_cmp_lt_u32_e64 %4, %2, %3\n\tv_cndmask_b32_e64 %3, %3, %0, %4\n\t"
+          "v_cmp_lt_u32_e64 %4, %1, %2\n\tv_cndmask_b32_e64 %0, %0, %1, %4\n\t"
+          "v_cmp_lt_u32_e64 %4, %3, %0\n\tv_cndmask_b32_e64 %2, %2, %3, %4\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=&s"(m));
+    } else if (KIND == 38) { // 4 x (v_cmp_e32 -> vcc, v_cndmask_b32_e32 on it at once)
+      asm volatile(
+          "v_cmp_lt_u32_e32 vcc, %0, %1\n\tv_cndmask_b32_e32 %1, %1, %2, vcc\n\t"
+          "v_cmp_lt_u32_e32 vcc, %2, %3\n\tv_cndmask_b32_e32 %3, %3, %0, vcc\n\t"
+          "v_cmp_lt_u32_e32 vcc, %1, %2\n\tv_cndmask_b32_e32 %0, %0, %1, vcc\n\t"
+          "v_cmp_lt_u32_e32 vcc, %3, %0\n\tv_cndmask_b32_e32 %2, %2, %3, vcc\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : : "vcc");
+    } else if (KIND == 39) { // 8 v_cndmask_b32_e64 with an inline-constant operand (0 / 1)
+      asm volatile(
+          "v_cndmask_b32_e64 %0, 0, %1, %4\n\tv_cndmask_b32_e64 %1, %2, 1, %5\n\t"
+          "v_cndmask_b32_e64 %2, 0, %3, %4\n\tv_cndmask_b32_e64 %3, %0, 1, %5\n\t"
+          "v_cndmask_b32_e64 %0, 0, %1, %5\n\tv_cndmask_b32_e64 %1, %2, 1, %4\n\t"
+          "v_cndmask_b32_e64 %2, 0, %3, %5\n\tv_cndmask_b32_e64 %3, %0, 1, %4\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d)
+          : "s"((uint64_t)s0 * 0x9E3779B97F4A7C15ull), "s"((uint64_t)s1 * 0xC2B2AE3D27D4EB4Full));
+    } else if (KIND == 40) { // 8 v_mov_b32_e32 from an SGPR
+      asm volatile(
+          "v_mov_b32_e32 %0, %4\n\tv_mov_b32_e32 %1, %5\n\tv_mov_b32_e32 %2, %4\n\t"
+          "v_mov_b32_e32 %3, %5\n\tv_mov_b32_e32 %0, %5\n\tv_mov_b32_e32 %1, %4\n\t"
+          "v_mov_b32_e32 %2, %5\n\tv_mov_b32_e32 %3, %4\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "s"(s0), "s"(s1));
+    } else if (KIND == 41) { // 8 v_lshl_or_b32 / v_add_lshl_u32 / v_lshl_add_u32
+      asm volatile(
+          "v_lshl_or_b32 %0, %1, 3, %2\n\tv_add_lshl_u32 %1, %2, %3, 2\n\t"
+          "v_lshl_add_u32 %2, %3, 1, %0\n\tv_lshl_or_b32 %3, %0, 5, %1\n\t"
+          "v_lshl_or_b32 %0, %1, 3, %2\n\tv_add_lshl_u32 %1, %2, %3, 2\n\t"
+          "v_lshl_add_u32 %2, %3, 1, %0\n\tv_lshl_or_b32 %3, %0, 5, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 42) { // 8 v_and_b32 with an SGPR operand (as the compiler emits for 64-bit masks)
+      asm volatile(
+          "v_and_b32_e32 %0, %4, %0\n\tv_and_b32_e32 %1, %5, %1\n\t"
+          "v_and_b32_e32 %2, %4, %2\n\tv_and_b32_e32 %3, %5, %3\n\t"
+          "v_and_b32_e32 %0, %5, %0\n\tv_and_b32_e32 %1, %4, %1\n\t"
+          "v_and_b32_e32 %2, %5, %2\n\tv_and_b32_e32 %3, %4, %3\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "s"(s0), "s"(s1));
     } else {                 // 4 VALU + 4 SALU interleaved
       asm volatile(
           "v_add_u32 %0, %0, %1\n\ts_add_u32 %4, %4, %5\n\tv_add_u32 %1, %1, %2\n\t"
@@ -353,5 +412,13 @@ int main() {
   run<32>("v_cmp->s_bcnt1 (8)", grid, out, clk);
   run<33>("v_writelane_b32", grid, out, clk);
   run<34>("v_ffbl_b32_e32", grid, out, clk);
+  run<35>("v_cndmask_e32 vcc const", grid, out, clk);
+  run<36>("v_cndmask_e64 vcc const", grid, out, clk);
+  run<37>("v_cmp_e64->cndmask (8)", grid, out, clk);
+  run<38>("v_cmp_e32->cndmask_e32 (8)", grid, out, clk);
+  run<39>("v_cndmask_e64 inline k", grid, out, clk);
+  run<40>("v_mov_b32 from sgpr", grid, out, clk);
+  run<41>("v_lshl_or/add_lshl/lshl_add", grid, out, clk);
+  run<42>("v_and_b32 sgpr (vop2)", grid, out, clk);
   return 0;
 }
