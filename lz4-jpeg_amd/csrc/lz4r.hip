@@ -27,7 +27,8 @@
 //            and it is LEFT-MAXIMAL (j == 0 or blk[j-1] != blk[p-1]): one
 //            v_xad + one compare of the two entries; a balanced lcp pass over
 //            the 4-gram keys takes the longest candidate per p, ties to the
-//            smallest j (LDS atomicMax).
+//            smallest j (LDS atomicMax of end << 19 | end << 9 | dist: the end
+//            twice, so that subtracting p << 9 later leaves the record word).
 //   blocked (lane l owns p = 5 l .. 5 l + 4):
 //     best   a candidate that is not left-maximal is the pair (j-1, p-1)
 //            shifted by one, whose match is one byte longer.  Hence
@@ -88,11 +89,6 @@
 // words, 32 = no header bytes.
 #ifndef LZ4R_VARIANT
 #define LZ4R_VARIANT 0
-#endif
-// LZ4R_PAIRS (tools builds only): lz4_pairs, two blocks per wave (DESIGN
-// §4.1: fewer instructions per block, slower at its 4-5 waves per SIMD)
-#ifndef LZ4R_PAIRS
-#define LZ4R_PAIRS 0
 #endif
 // LZ4R_PROF (tools builds only, like LZ4R_VARIANT): per-phase s_memtime
 // cycles of every wave summed into lz4r_prof[] (read by lz4r_prof_read).
@@ -166,7 +162,7 @@ struct TileLds {
     uint32_t ent[kArr];   // per position: link | tag << 17 | preceding byte << 22
     uint32_t word[kArr];  // then: the first match at or after x, as its record word
   };
-  uint32_t rec[kArr];     // local(p) accumulator: (p + len) << 9 | dist
+  uint32_t rec[kArr];     // local(p) accumulator: end << 19 | end << 9 | dist (end = p + len)
   // chain walkers: the walker's byte offset 4 p (candidate phase)
   __device__ __forceinline__ uint32_t *q() { return reinterpret_cast<uint32_t *>(buf + kQOff); }
   // per sequence, its match start (slow walk only)
@@ -548,7 +544,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
   // entries xor'ed, exactly when 2^15 <= x < 2^24 (bits 24..31 zero: the
   // tags agree; some bit 15..23 set: the preceding bytes differ or j == 0).
   // Candidates go to a list in S.cand, drained by a balanced lcp pass with
-  // LDS atomicMax into S.rec ((p + len) << 9 | (p - j): the longest, ties to
+  // LDS atomicMax into S.rec (end << 19 | end << 9 | (p - j), end = p + len:
+  // the longest, ties to
   // the smallest j).
   uint32_t longm = 0;                    // this lane verified a candidate of >= 256 bytes
   if (search && LZ4R_VARIANT != 3) {
@@ -575,7 +572,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
         if (LZ4R_VARIANT == 5) {          // ablation: the lcp without its result
           if (l == 12345) S.rec[0] = 1u;
         } else if (l >= 4) {
-          atomicMax(&S.rec[p], ((uint32_t)(p + l) << 9) | (uint32_t)(p - j));
+          // end << 19 | end << 9 | dist (the end twice: see the word pass)
+          atomicMax(&S.rec[p], (uint32_t)(p + l) * 0x80200u | (uint32_t)(p - j));
         }
         longm |= l >= 256 ? 1u : 0u;     // (a match the uint8_t return truncates)
       }
@@ -647,7 +645,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
   uint32_t v[5];
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
-    // local(p) as end << 9 | dist; 0 without a candidate and at and past n
+    // local(p) as end << 19 | end << 9 | dist; 0 without a candidate and at
+    // and past n
     v[r] = S.rec[p0 + r];
     if (r) v[r] = max(v[r], v[r - 1]);
   }
@@ -663,38 +662,44 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int p = p0 + r;
-      const int len = (int)(v[r] >> 9) - p;
+      const int len = (int)(v[r] >> 19) - p;
       if (p < n) mout[p] = len >= 4 ? (uint32_t)len | ((v[r] & 511u) << 16) : 0u;
     }
     return 0;
   }
-  // x = v - p << 9 = len << 9 | dist (len <= 0, i.e. x < 512 or negative,
-  // where no match covers p); M = len & 0xFF (the uint8_t return, LZ4.c:317).
-  // A match starts at p when len >= 4 and M != 0 (len 256 is a literal,
-  // LZ4.c:521).
+  // The scan values are end << 19 | end << 9 | dist (the lexicographic order
+  // of (end, dist): the middle copy follows the end), so x = v - p << 9 =
+  // end << 19 | len << 9 | dist; a match covers p when end >= p + 4 (one
+  // compare of the scan value), and M = len & 0xFF (the uint8_t return,
+  // LZ4.c:317).  A match starts at p when len >= 4 and M != 0 (len 256 is a
+  // literal, LZ4.c:521).
   // The greedy parse (LZ4.c:516-583) at x -- 0, then the end of the previous
   // match -- takes the first matchable position c = nm(x) >= x with its M and
   // dist.  word[x] holds exactly that, as the match's own record word
-  //   dist | M << 9 | 4 (c + M) << 17
-  // whose top field is the byte offset of the next word the walk reads, or
-  // kWordEnd when no match starts at or after x.  So the walk reads one word
-  // per sequence and needs no successor table (no gathers, no second array).
+  //   dist | M << 9 | (c + M) << 19
+  // -- x itself when the match is not truncated (len < 256) -- whose top
+  // field, as the shifted word >> 17 = 4 (c + M), is the byte offset of the
+  // next word the walk reads, or kWordEnd when no match starts at or after x.
+  // So the walk reads one word per sequence and needs no successor table (no
+  // gathers, no second array).
   // (the word pass is instantiated for both cases below, so the match flags
   // stay lane masks in SGPRs: merged across a branch they were packed into
   // a VGPR and unpacked again, ~15 VALU)
   const uint32_t nP9 = 0u - ((uint32_t)p0 << 9);
+  const uint32_t K0 = (uint32_t)(p0 + 4) << 19;
   auto word_pass = [&](auto fast) -> uint32_t {
     uint32_t rw[5];               // p's own word (where a match starts at p)
     bool mt[5];                   // a match starts at p (len >= 4, M != 0)
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const uint32_t x = v[r] + nP9 + (0u - ((uint32_t)r << 9));   // one v_add3
+      const bool m4 = v[r] >= K0 + ((uint32_t)r << 19);             // len >= 4
       if constexpr (decltype(fast)::value) {
-        mt[r] = (int)x >= (4 << 9);
-        rw[r] = ((v[r] << 10) & 0xFFF80000u) | (x & 0x7FFFFu);   // one v_bfi
+        mt[r] = m4;
+        rw[r] = x;
       } else {
         const uint32_t M = __builtin_amdgcn_ubfe(x, 9, 8);
-        mt[r] = (int)x >= (4 << 9) && M != 0u;
+        mt[r] = m4 && M != 0u;
         rw[r] = ((M + (uint32_t)(p0 + r)) << 19) | (x & 0x1FFFFu);
       }
     }
@@ -718,12 +723,13 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
   };
   // No verified candidate reached 256 bytes, so no best(p) does (a scan term
   // is a candidate shifted right, never longer): len < 256, M = len, every
-  // len >= 4 is a match, and the word's field c + M is the scan value's end:
-  // rw = (end << 19) | (len << 9 | dist), the shifted scan value over x by one
-  // v_bfi (x's bits 17..18 are len's bits 8..9: zero).  Otherwise the general
-  // form (M = len & 0xFF, len 256 no match).
-  const uint32_t w0 = ballot(longm != 0u) ? word_pass(std::false_type{})
-                                           : word_pass(std::true_type{});
+  // len >= 4 is a match, and the word is x (its bits 17..18, len's bits
+  // 8..9, are zero).  Otherwise the general form (M = len & 0xFF, len 256 no
+  // match).  The records rounds are instantiated the same way: without a
+  // truncated match no M is 1..3, so a sequence's size field is its byte
+  // count and one plain wave sum gives both.
+  const bool fastw = !ballot(longm != 0u);   // no truncated match: M = len, never 1..3
+  const uint32_t w0 = fastw ? word_pass(std::true_type{}) : word_pass(std::false_type{});
   wave_sync();
 
   PROF_MARK(4);                       // word
@@ -806,31 +812,40 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
   // one round: sequence kk = s0 + lane has the match word wv (n << 19 -- no
   // match, M = dist = 0, ending at n -- past the matches); returns false once
   // the round holds the last sequence
-  auto round = [&](int kk, uint32_t wv) {
+  auto round = [&](auto fast, int kk, uint32_t wv) {
     const int M = (int)((wv >> 9) & 255u);
     const int end = (int)(wv >> 19);
     const uint32_t cq = (uint32_t)(end - M);                       // the match start
-    const bool ism = (int)cq < n;                                  // ends with a match
-    const int nm_r = __popcll(ballot(ism));                        // a prefix of the round
+    const uint64_t ismm = ballot((int)cq < n);                     // ends with a match
+    const int nm_r = __popcll(ismm);                               // a prefix of the round
     const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);   // wave_shr:1
     const int pend = lane == 0 ? end_prev : (int)upv;             // literal run start
     end_prev = (int)lane63((uint32_t)end);
     const int L = (int)cq - pend;
     // + the tail (lane nm_r, when literals are left); the mask from ballots
     // of the compares (a ballot of a combined bool costs two VALU)
-    const uint64_t am = ballot(ism) | (ballot(lane == nm_r) & ballot(pend < n));
+    const uint64_t am = ismm | (ballot(lane == nm_r) & ballot(pend < n));
     // bytes written (LZ4.c:365-413) | the size field (LZ4.c:546-575) << 16:
     // 5 + L + the literal-extension bytes (one from 15, two at L = 270, where
     // the uint8_t remainder is 255: LZ4.c:376-385) + a match-extension byte
     // (M >= 19); the size field also counts one for M = 1..3, which
     // write_sequence never writes (LZ4.c:393 vs :562-575)
-    uint32_t ws = (uint32_t)(L + 5 + (L >= 15 ? 1 : 0) + (L == 270 ? 1 : 0)) * 0x10001u;
-    ws += M >= 19 ? 0x10001u : 0u;
-    ws += (uint32_t)(M - 1) < 3u ? 0x10000u : 0u;
-    const uint32_t tot = lane63(wave_incl_add(sel_mask(am, ws, 0u)));
+    if constexpr (decltype(fast)::value) {
+      // no M = 1..3 (no truncated match): the size fields are the bytes
+      const uint32_t ws = (uint32_t)(L + 5) + (L >= 15 ? 1u : 0u) + (L == 270 ? 1u : 0u) +
+                          (M >= 19 ? 1u : 0u);
+      const uint32_t tot = lane63(wave_incl_add(sel_mask(am, ws, 0u)));
+      ocar += (int)tot;
+      szsum += (int)tot;
+    } else {
+      uint32_t ws = (uint32_t)(L + 5 + (L >= 15 ? 1 : 0) + (L == 270 ? 1 : 0)) * 0x10001u;
+      ws += M >= 19 ? 0x10001u : 0u;
+      ws += (uint32_t)(M - 1) < 3u ? 0x10000u : 0u;
+      const uint32_t tot = lane63(wave_incl_add(sel_mask(am, ws, 0u)));
+      ocar += (int)(tot & 0xFFFFu);
+      szsum += (int)(tot >> 16);
+    }
     store_lanes1(am, recs, 4u * (uint32_t)kk, wv);   // recs[1 + kk]: the sequence's word (the tail: n << 19)
-    ocar += (int)(tot & 0xFFFFu);
-    szsum += (int)(tot >> 16);
     nseq += (int)__popcll(am);
     return nm_r == 64;
   };
@@ -839,12 +854,18 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
     // register wrapped) come from the redone walk in S.seq
     const uint32_t wtail = (uint32_t)n << 19;
     const uint32_t c0 = slow ? S.seq()[lane] : (lane < it ? seqv : wtail);
-    if (round(lane, c0)) {             // 64 match sequences: the tail or more follow
-      for (int s0 = 64;; s0 += 64) {
-        const int kk = s0 + lane;
-        if (!round(kk, slow && kk < Sv_slow ? S.seq()[kk] : wtail)) break;
+    auto rounds = [&](auto fast) {
+      if (round(fast, lane, c0)) {     // 64 match sequences: the tail or more follow
+        for (int s0 = 64;; s0 += 64) {
+          const int kk = s0 + lane;
+          if (!round(fast, kk, slow && kk < Sv_slow ? S.seq()[kk] : wtail)) break;
+        }
       }
-    }
+    };
+    if (fastw)
+      rounds(std::true_type{});
+    else
+      rounds(std::false_type{});
   }
   PROF_MARK(6);                       // records
   if (lane == 0) recs[0] = (uint32_t)szsum | ((uint32_t)nseq << 16);
@@ -891,470 +912,6 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   }
 }
 
-#if LZ4R_PAIRS
-// ---- lz4_pairs: two blocks per wave (tools-only A/B, LZ4R_PAIRS=1) ---------
-// The same match finder, greedy parse and records as encode_block, for the
-// two adjacent full blocks A = 2u and B = 2u + 1 in one wave: every lane owns
-// positions of both (position-major p = 64 r + lane of A and of B for the
-// index and the walk; blocked idx 10 lane .. 10 lane + 9 over the combined
-// 640-entry arrays, A at 0..319 and B at 320..639, for the scans), so the
-// per-wave work that does not grow with the positions is paid once for two
-// blocks: the walkers of both blocks share the walk passes and the takes,
-// their candidates one lcp drain, one max-scan and one suffix pass serve both
-// (B's scan values carry an offset above every A value, and the suffix stops
-// at the half boundary), the two greedy walks advance in one loop (one LDS
-// read, the halves of the wave reading their own block's word), and both
-// blocks' records leave in one round (A's sequences on lanes 0..31, B's on
-// 32..63).  8 KB of LDS per wave: 5 waves per SIMD, 10 blocks in flight per
-// SIMD (the one-block kernel: 8).
-//
-// LDS (bytes): two 1024-bucket head tables [0, 8192) during the index; then
-// the entries [0, 2560) (then the 4-gram keys for the lcp drain, then the
-// match words), the local(p) accumulators [2560, 5120), the walker queue as
-// u16 byte offsets [5120, 6448) and the candidates [6448, 6960).
-constexpr int kPPos = 2 * kArr;                 // 640 entries per array
-constexpr int kPEntOff = 0;                     // entries, then keys, then the match words
-constexpr int kPRecOff = kPEntOff + 4 * kPPos;  // 2560
-constexpr int kPQOff = kPRecOff + 4 * kPPos;    // 5120: u16 walker queue
-constexpr int kPQ = 2 * kBlk + 64;              // 664 entries (reads run to 63 past the last)
-constexpr int kPCandOff = kPQOff + 2 * kPQ;     // 6448
-constexpr int kPLds = 8192;
-static_assert(kPCandOff + 4 * kCand <= kPLds && kPCandOff % 16 == 0 && kPRecOff % 16 == 0,
-              "pair LDS layout");
-constexpr uint32_t kPNoLink = 4092;             // 12-bit link field of kEmptyHead
-static_assert((kEmptyHead & 0xFFFu) == kPNoLink && kPNoLink >= 4 * kPPos, "pair chain end");
-constexpr uint32_t kPOff = 1u << 20;            // B's scan offset: above every (end << 9 | dist)
-
-// 10 empties, then 10 exchanges (A's five rows, B's five), one wait
-__device__ __forceinline__ void xchg_rtn10(uint32_t (&old)[10], const uint32_t (&a)[10],
-                                           const uint32_t (&v)[10]) {
-  asm volatile(
-      "ds_write_b32 %10, %30\n\tds_write_b32 %11, %30\n\tds_write_b32 %12, %30\n\t"
-      "ds_write_b32 %13, %30\n\tds_write_b32 %14, %30\n\tds_write_b32 %15, %30\n\t"
-      "ds_write_b32 %16, %30\n\tds_write_b32 %17, %30\n\tds_write_b32 %18, %30\n\t"
-      "ds_write_b32 %19, %30\n\t"
-      "ds_wrxchg_rtn_b32 %0, %10, %20\n\tds_wrxchg_rtn_b32 %1, %11, %21\n\t"
-      "ds_wrxchg_rtn_b32 %2, %12, %22\n\tds_wrxchg_rtn_b32 %3, %13, %23\n\t"
-      "ds_wrxchg_rtn_b32 %4, %14, %24\n\tds_wrxchg_rtn_b32 %5, %15, %25\n\t"
-      "ds_wrxchg_rtn_b32 %6, %16, %26\n\tds_wrxchg_rtn_b32 %7, %17, %27\n\t"
-      "ds_wrxchg_rtn_b32 %8, %18, %28\n\tds_wrxchg_rtn_b32 %9, %19, %29\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(old[0]), "=&v"(old[1]), "=&v"(old[2]), "=&v"(old[3]), "=&v"(old[4]),
-        "=&v"(old[5]), "=&v"(old[6]), "=&v"(old[7]), "=&v"(old[8]), "=&v"(old[9])
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]),
-        "v"(a[7]), "v"(a[8]), "v"(a[9]), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]),
-        "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]), "v"(v[9]), "v"(kEmptyHead)
-      : "memory");
-}
-
-// ent[320 h + 64 r + lane] = e[5 h + r] and rec[0 .. 640) = 0: 20 add-TID
-// stores, one m0 set (after the heads' last exchange: both lie under them)
-__device__ __forceinline__ void pair_ent_rec_addtid(const uint32_t (&e)[10]) {
-  asm volatile(
-      "s_mov_b32 m0, 0\n\t"
-      "s_nop 0\n\t"
-      "ds_write_addtid_b32 %0 offset:%c11\n\tds_write_addtid_b32 %1 offset:%c12\n\t"
-      "ds_write_addtid_b32 %2 offset:%c13\n\tds_write_addtid_b32 %3 offset:%c14\n\t"
-      "ds_write_addtid_b32 %4 offset:%c15\n\tds_write_addtid_b32 %5 offset:%c16\n\t"
-      "ds_write_addtid_b32 %6 offset:%c17\n\tds_write_addtid_b32 %7 offset:%c18\n\t"
-      "ds_write_addtid_b32 %8 offset:%c19\n\tds_write_addtid_b32 %9 offset:%c20\n\t"
-      "ds_write_addtid_b32 %10 offset:%c21\n\tds_write_addtid_b32 %10 offset:%c22\n\t"
-      "ds_write_addtid_b32 %10 offset:%c23\n\tds_write_addtid_b32 %10 offset:%c24\n\t"
-      "ds_write_addtid_b32 %10 offset:%c25\n\tds_write_addtid_b32 %10 offset:%c26\n\t"
-      "ds_write_addtid_b32 %10 offset:%c27\n\tds_write_addtid_b32 %10 offset:%c28\n\t"
-      "ds_write_addtid_b32 %10 offset:%c29\n\tds_write_addtid_b32 %10 offset:%c30"
-      :
-      : "v"(e[0]), "v"(e[1]), "v"(e[2]), "v"(e[3]), "v"(e[4]), "v"(e[5]), "v"(e[6]),
-        "v"(e[7]), "v"(e[8]), "v"(e[9]), "v"(0u),
-        "i"(kPEntOff), "i"(kPEntOff + 256), "i"(kPEntOff + 512), "i"(kPEntOff + 768),
-        "i"(kPEntOff + 1024), "i"(kPEntOff + 1280), "i"(kPEntOff + 1536), "i"(kPEntOff + 1792),
-        "i"(kPEntOff + 2048), "i"(kPEntOff + 2304),
-        "i"(kPRecOff), "i"(kPRecOff + 256), "i"(kPRecOff + 512), "i"(kPRecOff + 768),
-        "i"(kPRecOff + 1024), "i"(kPRecOff + 1280), "i"(kPRecOff + 1536), "i"(kPRecOff + 1792),
-        "i"(kPRecOff + 2048), "i"(kPRecOff + 2304)
-      : "memory");
-}
-
-// key[320 h + 64 r + lane] = k[5 h + r] over the entries (dead after the
-// walk), one m0 set
-__device__ __forceinline__ void pair_keys_addtid(const uint32_t (&k)[10]) {
-  asm volatile(
-      "s_mov_b32 m0, 0\n\t"
-      "s_nop 0\n\t"
-      "ds_write_addtid_b32 %0 offset:%c10\n\tds_write_addtid_b32 %1 offset:%c11\n\t"
-      "ds_write_addtid_b32 %2 offset:%c12\n\tds_write_addtid_b32 %3 offset:%c13\n\t"
-      "ds_write_addtid_b32 %4 offset:%c14\n\tds_write_addtid_b32 %5 offset:%c15\n\t"
-      "ds_write_addtid_b32 %6 offset:%c16\n\tds_write_addtid_b32 %7 offset:%c17\n\t"
-      "ds_write_addtid_b32 %8 offset:%c18\n\tds_write_addtid_b32 %9 offset:%c19"
-      :
-      : "v"(k[0]), "v"(k[1]), "v"(k[2]), "v"(k[3]), "v"(k[4]), "v"(k[5]), "v"(k[6]),
-        "v"(k[7]), "v"(k[8]), "v"(k[9]),
-        "i"(kPEntOff), "i"(kPEntOff + 256), "i"(kPEntOff + 512), "i"(kPEntOff + 768),
-        "i"(kPEntOff + 1024), "i"(kPEntOff + 1280), "i"(kPEntOff + 1536), "i"(kPEntOff + 1792),
-        "i"(kPEntOff + 2048), "i"(kPEntOff + 2304)
-      : "memory");
-}
-
-// Encode blocks A (300 B at g) and B (the 300 B after it; both full, and
-// bytes past B readable: B is not the launch's last block) as records at
-// recs (A's slot; B's is the next) and return their stream bytes in WA, WB.
-__device__ __forceinline__ void encode_pair(uint8_t *__restrict__ L, const uint8_t *__restrict__ g,
-                                            uint32_t *__restrict__ recs,
-                                            uint32_t *__restrict__ status, int &WA, int &WB) {
-  constexpr int n = kBlk;
-  const int lane = threadIdx.x;
-  const int hf = lane >> 5;                     // the blocked layout's half: 0 = A, 1 = B
-  auto u32at = [&](int off) -> uint32_t & { return *reinterpret_cast<uint32_t *>(L + off); };
-
-  // ---- index: per block, per-bucket chains of its 4-gram starts -----------
-  // As encode_block: k = 5 h + r is position p = 64 r + lane of block h, its
-  // entry at idx = 320 h + p (byte offset 4 idx, a 12-bit link); block h's
-  // heads are table h (4096 h + 4 bucket).  Positions are inserted in
-  // ascending idx, so every chain strictly decreases within its block.
-  bool walk[10];
-  uint32_t key[10];
-  uint32_t qn = 0;
-  {
-    const uint32_t sh = (uint32_t)lane & 3u;
-    const uint32_t *bw = reinterpret_cast<const uint32_t *>(g) + (lane >> 2);
-    uint32_t pt[10], adr[10], set[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      const int h = k / 5, r = k % 5;
-      const uint32_t w1 = bw[75 * h + 16 * r], w2 = bw[75 * h + 16 * r + 1];
-      key[k] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-    }
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      const int h = k / 5, r = k % 5;
-      const uint32_t below = r ? (uint32_t)__builtin_amdgcn_readlane((int)key[k - 1], 63) : 0u;
-      const uint32_t pb = (uint32_t)__builtin_amdgcn_update_dpp((int)below, (int)key[k], 0x138,
-                                                               0xf, 0xf, false);
-      const uint32_t hv = key[k] * 2654435761u;
-      pt[k] = __builtin_amdgcn_perm(pb, hv, 0x02040C0Cu);
-      // Row 4's lanes 41..63 (p >= 297) start no 4-gram.  They still
-      // exchange into their own table (no dummy heads: no LDS past the
-      // tables) as the last positions of it, so no chain ever reaches them,
-      // and they are never walkers.
-      adr[k] = ((hv >> (32 - kHB)) << 2) + 4096u * h;
-      set[k] = (uint32_t)(4 * (320 * h + 64 * r + lane));
-    }
-    if (lane == 0) {
-      pt[0] |= 1u << 15;
-      pt[5] |= 1u << 15;
-    }
-    uint32_t old[10];
-    xchg_rtn10(old, adr, set);
-    uint32_t e[10];
-    int d[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      e[k] = (old[k] & 0xFFFu) | pt[k];
-      walk[k] = (int)old[k] >= 0 && (k % 5 < 4 || lane < 41);
-      d[k] = (int)(old[k] - set[k]);
-    }
-    const int y = max(max(max(max(d[0], d[1]), max(d[2], d[3])), max(max(d[4], d[5]), d[6])),
-                      max(max(d[7], d[8]), d[9]));
-    if (ballot(y >= 0)) atomicOr(status, 1u);
-    // queue: rows from r = 4 down, B before A within a row
-#pragma unroll
-    for (int r = 4; r >= 0; --r) {
-#pragma unroll
-      for (int h = 1; h >= 0; --h) {
-        const int k = 5 * h + r;
-        const uint64_t m = ballot(walk[k]);
-        // (u16 queue; a lane without a walker writes its own idle word of
-        // the candidate list)
-        const uint32_t at = sel_mask(m, (rank_below_plus(m, qn) << 1) + kPQOff,
-                                     (uint32_t)(kPCandOff + 4 * lane));
-        *reinterpret_cast<uint16_t *>(L + at) = (uint16_t)set[k];
-        qn += (uint32_t)__popcll(m);
-      }
-    }
-    pair_ent_rec_addtid(e);
-  }
-  wave_sync();
-  const int qwr = (int)qn;
-  wave_sync();
-
-  // ---- candidates: the walkers of both blocks share the passes -------------
-  {
-    constexpr int kTrash = kCand - 1;
-    int ncand = 0;
-    auto ent_at = [&](int off) { return u32at(kPEntOff + off); };
-    auto drain = [&](auto keys) {
-      constexpr bool kKeys = decltype(keys)::value;
-      wave_sync();
-      for (int i = lane; i < ncand; i += 64) {
-        const uint32_t pr = u32at(kPCandOff + 4 * i);
-        const int pi = (int)(pr & 0xFFFFu) >> 2, ji = (int)(pr >> 18);   // idx, ji < pi
-        const int h = pi >= 320 ? 1 : 0;
-        const int p = pi - 320 * h, j = ji - 320 * h;
-        const int l = kKeys ? lcp_keys(reinterpret_cast<const uint32_t *>(L + kPEntOff) + ji,
-                                       reinterpret_cast<const uint32_t *>(L + kPEntOff) + pi, n - p)
-                            : lcp_global(g + 300 * h + j, g + 300 * h + p, n - p);
-        if (l >= 4)
-          atomicMax(&u32at(kPRecOff + 4 * pi), ((uint32_t)(p + l) << 9) | (uint32_t)(p - j));
-      }
-      wave_sync();
-    };
-    int qrd2 = 0;
-    const int qwr2 = 2 * qwr;
-    int a = 0, b = 0;
-    uint32_t me = 0;
-    uint64_t vm = 0;
-    auto pass = [&]() {
-      const uint32_t o = ent_at(b);
-      const uint64_t cm = vm & ballot(((me ^ o) - (1u << 15)) < (1u << 24) - (1u << 15));
-      const int sl4 =
-          (int)sel_mask(cm, (uint32_t)(4 * ncand + (rank_below(cm) << 2)), (uint32_t)(4 * kTrash));
-      u32at(kPCandOff + sl4) = (uint32_t)a | ((uint32_t)b << 16);
-      ncand += __popcll(cm);
-      const int bn = (int)(o & 4095u);
-      vm &= ballot(bn < b);
-      b = bn;
-      if (ncand > kTrash - 64) {
-        drain(std::false_type{});
-        ncand = 0;
-      }
-    };
-    while (qrd2 < qwr2) {
-      const uint64_t em = ~vm;
-      const int idx2 = qrd2 + (rank_below(em) << 1);
-      const uint64_t nm_ = em & ballot(idx2 < qwr2);
-      const uint32_t it = *reinterpret_cast<const uint16_t *>(L + kPQOff + idx2);
-      a = (int)sel_mask(nm_, it, (uint32_t)a);
-      vm |= nm_;
-      qrd2 += 2 * __popcll(em);
-      me = ent_at(a);
-      b = (int)sel_mask(nm_, me & 4095u, (uint32_t)b);
-      pass();
-    }
-    while (vm) {
-      pass();
-      if (!vm) break;
-      pass();
-    }
-    if (ncand) {
-      pair_keys_addtid(key);
-      drain(std::true_type{});
-    }
-  }
-  wave_sync();
-
-  // ---- best(p): one max-scan over the combined blocked layout --------------
-  // lane l owns idx 10 l .. 10 l + 9: lanes 0..31 block A, 32..63 block B
-  // (position pos0 + r, pos0 = 10 (l mod 32)); B's values carry kPOff, above
-  // every A value, so B's prefix never takes one of A's
-  const int pos0 = 10 * (lane & 31);
-  const uint32_t hoff = hf ? kPOff : 0u;
-  uint32_t v[10];
-  {
-    const uint2 *rp = reinterpret_cast<const uint2 *>(L + kPRecOff) + 5 * lane;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const uint2 x = rp[i];                    // ds_read_b64 (8-B aligned: 40 B per lane)
-      v[2 * i] = x.x + hoff;
-      v[2 * i + 1] = x.y + hoff;
-    }
-#pragma unroll
-    for (int r = 1; r < 10; ++r) v[r] = max(v[r], v[r - 1]);
-    const uint32_t incl = wave_incl_max(v[9]);
-    const uint32_t excl = dpp<0x138, 0xf, 0xf>(incl);
-#pragma unroll
-    for (int r = 0; r < 10; ++r) v[r] = max(v[r], excl);
-  }
-  uint32_t rw[10];
-  bool mt[10];
-  {
-    const uint32_t nP9 = 0u - ((uint32_t)pos0 << 9) - hoff;
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-      const uint32_t x = v[r] + nP9 + (0u - ((uint32_t)r << 9));
-      const uint32_t M = (x >> 9) & 255u;
-      mt[r] = (int)x >= (4 << 9) && M != 0u;
-      // field 4 (idx of c + M) = 4 (320 h + c + M)
-      rw[r] = ((M + (uint32_t)(320 * hf + pos0 + r)) << 19) | (x & 0x1FFFFu);
-    }
-  }
-  // ---- the match words, the suffix stopping at the half boundary ----------
-  const uint32_t wend = (uint32_t)(4 * (320 * hf + kArr - 1)) << 17;   // word[319 / 639]
-  uint32_t w0A, w0B;
-  {
-    uint32_t loc = wend;
-#pragma unroll
-    for (int r = 9; r >= 0; --r) loc = mt[r] ? rw[r] : loc;
-    const uint64_t has = ballot(loc != wend);
-    const uint64_t half = lane < 32 ? 0xFFFFFFFFull : ~0ull;
-    const uint64_t up = has & ~((2ull << lane) - 1ull) & half;
-    const int src = up ? ctz64(up) : lane;
-    const uint32_t nx = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)loc);
-    uint32_t w = up ? nx : wend;
-    uint32_t wr[10];
-#pragma unroll
-    for (int r = 9; r >= 0; --r) wr[r] = w = mt[r] ? rw[r] : w;
-    uint2 *wp = reinterpret_cast<uint2 *>(L + kPEntOff) + 5 * lane;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) wp[i] = make_uint2(wr[2 * i], wr[2 * i + 1]);
-    w0A = (uint32_t)__builtin_amdgcn_readlane((int)wr[0], 0);
-    w0B = (uint32_t)__builtin_amdgcn_readlane((int)wr[0], 32);
-  }
-  wave_sync();
-
-  // ---- both greedy walks in one loop ----------------------------------------
-  // lanes 0..31 read A's next word, 32..63 B's (each half one address); the
-  // words go to lane k (A) and lane k + 32 (B) of seqv while both fit; a
-  // finished walk stays on its end word (word[319] / word[639] is itself).
-  const uint32_t limA = (uint32_t)(4 * n + 1) << 17;
-  const uint32_t limB = (uint32_t)(4 * (320 + n) + 1) << 17;
-  int it = 0;
-  uint32_t seqv = 0xFFFFFFFFu;
-  if (w0A < limA || w0B < limB) {
-    uint32_t wa = w0A, wb = w0B, vt;
-    uint32_t va = (lane < 32 ? w0A : w0B) >> 17;
-    // (v_writelane takes one SGPR besides m0: B's lane select is m0 + 32,
-    // set and undone around its write; an s_nop keeps the SALU write of m0
-    // two instructions ahead of its use as a lane select)
-    asm volatile(
-        "s_mov_b32 m0, 0\n"
-        "1:\n\t"
-        "v_writelane_b32 %0, %1, m0\n\t"
-        "s_add_u32 m0, m0, 32\n\t"
-        "ds_read_b32 %4, %3 offset:%c8\n\t"
-        "s_nop 0\n\t"
-        "v_writelane_b32 %0, %2, m0\n\t"
-        "s_sub_u32 m0, m0, 31\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_readfirstlane_b32 %1, %4\n\t"
-        "v_readlane_b32 %2, %4, 32\n\t"
-        "v_lshrrev_b32 %3, 17, %4\n\t"
-        "s_cmp_lt_u32 %1, %6\n\t"
-        "s_cbranch_scc1 1b\n\t"
-        "s_cmp_lt_u32 %2, %7\n\t"
-        "s_cbranch_scc1 1b\n\t"
-        "s_mov_b32 %5, m0"
-        : "+v"(seqv), "+s"(wa), "+s"(wb), "+v"(va), "=&v"(vt), "=s"(it)
-        : "s"(limA), "s"(limB), "i"(kPEntOff)
-        : "scc", "memory");
-  }
-  // ---- records ---------------------------------------------------------------
-  int ocarA = 3, ocarB = 3;
-  uint32_t hdrA = 0, hdrB = 0;
-  if (it <= 31) {
-    // one round, A's sequences on lanes 0..31 and B's on 32..63 (kk = lane
-    // within the half; lane kk >= the block's count: the tail, or nothing)
-    const int kk = lane & 31;
-    const uint32_t lim = hf ? limB : limA;
-    const uint32_t wv = seqv < lim ? seqv : (uint32_t)(320 * hf + n) << 19;
-    const int M = (int)((wv >> 9) & 255u);
-    const int end = (int)(wv >> 19) - 320 * hf;
-    const int cq = end - M;
-    const bool ism = cq < n;
-    const uint64_t ismm = ballot(ism);
-    const uint64_t hm = hf ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
-    const int nm_r = __popcll(ismm & hm);                  // the half's match sequences
-    const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);
-    const int pend = kk == 0 ? 0 : (int)upv;
-    const int Lr = cq - pend;
-    const uint64_t am = ismm | (ballot(kk == nm_r) & ballot(pend < n));
-    uint32_t ws = (uint32_t)(Lr + 5 + (Lr >= 15 ? 1 : 0) + (Lr == 270 ? 1 : 0)) * 0x10001u;
-    ws += M >= 19 ? 0x10001u : 0u;
-    ws += (uint32_t)(M - 1) < 3u ? 0x10000u : 0u;
-    const uint32_t incl = wave_incl_add(sel_mask(am, ws, 0u));
-    const uint32_t totA = (uint32_t)__builtin_amdgcn_readlane((int)incl, 31);
-    const uint32_t totB = lane63(incl) - totA;
-    if (sel_mask(am, 1u, 0u))
-      recs[hf * (kSlot / 4) + 1 + kk] = wv - (hf ? 320u << 19 : 0u);
-    ocarA += (int)(totA & 0xFFFFu);
-    ocarB += (int)(totB & 0xFFFFu);
-    hdrA = (totA >> 16) | ((uint32_t)__popcll(am & 0xFFFFFFFFull) << 16);
-    hdrB = (totB >> 16) | ((uint32_t)__popcll(am >> 32) << 16);
-  } else {
-    // more than 31 sequences in a block (rare: short or truncated matches):
-    // redo each walk into a list over the dead accumulators and emit each
-    // block in full-width rounds, as encode_block
-    uint32_t *const sq = reinterpret_cast<uint32_t *>(L + kPRecOff);   // (dead after the scan)
-    int cnt[2] = {0, 0};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t lim = h ? limB : limA;
-      int c = 0;
-      for (uint32_t w = h ? w0B : w0A; w < lim;
-           w = (uint32_t)__builtin_amdgcn_readfirstlane((int)u32at(kPEntOff + (int)(w >> 17)))) {
-        if (lane == 0) sq[320 * h + c] = w;
-        ++c;
-      }
-      cnt[h] = c;
-    }
-    wave_sync();
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      int nseq = 0, ocar = 3, szsum = 0, end_prev = 0;
-      const uint32_t wtail = (uint32_t)(320 * h + n) << 19;
-      for (int s0 = 0;; s0 += 64) {
-        const int kq = s0 + lane;
-        const uint32_t wv = kq < cnt[h] ? sq[320 * h + kq] : wtail;
-        const int M = (int)((wv >> 9) & 255u);
-        const int end = (int)(wv >> 19) - 320 * h;
-        const int cq = end - M;
-        const bool ism = cq < n;
-        const int nm_r = __popcll(ballot(ism));
-        const uint32_t upv = dpp<0x138, 0xf, 0xf>((uint32_t)end);
-        const int pend = lane == 0 ? end_prev : (int)upv;
-        end_prev = (int)lane63((uint32_t)end);
-        const int Lr = cq - pend;
-        const uint64_t am = ballot(ism) | (ballot(lane == nm_r) & ballot(pend < n));
-        uint32_t ws = (uint32_t)(Lr + 5 + (Lr >= 15 ? 1 : 0) + (Lr == 270 ? 1 : 0)) * 0x10001u;
-        ws += M >= 19 ? 0x10001u : 0u;
-        ws += (uint32_t)(M - 1) < 3u ? 0x10000u : 0u;
-        const uint32_t tot = lane63(wave_incl_add(sel_mask(am, ws, 0u)));
-        if (sel_mask(am, 1u, 0u))
-          recs[h * (kSlot / 4) + 1 + kq] = wv - (h ? 320u << 19 : 0u);
-        ocar += (int)(tot & 0xFFFFu);
-        szsum += (int)(tot >> 16);
-        nseq += (int)__popcll(am);
-        if (nm_r != 64) break;
-      }
-      if (h == 0) {
-        ocarA = ocar;
-        hdrA = (uint32_t)szsum | ((uint32_t)nseq << 16);
-      } else {
-        ocarB = ocar;
-        hdrB = (uint32_t)szsum | ((uint32_t)nseq << 16);
-      }
-    }
-  }
-  if (lane == 0) recs[0] = hdrA;
-  if (lane == 32) recs[kSlot / 4] = hdrB;
-  WA = ocarA;
-  WB = ocarB;
-}
-
-// lz4_pairs: workgroup = one wave = blocks 2u and 2u + 1 (u < npairs: both
-// full, and B is not the launch's last block); XCD-aware order over the
-// pairs as lz4_tiles.  The launch's remaining one or two blocks go to
-// lz4_tiles.
-__global__ __launch_bounds__(64) void lz4_pairs(const uint8_t *__restrict__ in, uint32_t npairs,
-                                                uint32_t per, uint8_t *__restrict__ slots,
-                                                uint32_t *__restrict__ usz,
-                                                uint16_t *__restrict__ bsizes,
-                                                uint32_t *__restrict__ status) {
-  __shared__ alignas(16) uint8_t L[kPLds];
-  const int lane = threadIdx.x;
-  const uint32_t u = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-  if (u >= npairs) return;
-  const size_t t = 2 * (size_t)u;
-  uint32_t *const recs = reinterpret_cast<uint32_t *>(slots + t * kSlot);
-  int WA, WB;
-  encode_pair(L, in + t * kBlk, recs, status, WA, WB);
-  if (lane == 0) {
-    usz[t] = (uint32_t)WA;
-    usz[t + 1] = (uint32_t)WB;
-    bsizes[t] = (uint16_t)WA;
-    bsizes[t + 1] = (uint16_t)WB;
-  }
-}
-#endif  // LZ4R_PAIRS
 
 // Per-position longest matches of every block (the batch form of
 // find_longest_match): the same staging and match finder as lz4_tiles.
@@ -1780,7 +1337,6 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
 // left in *d_len; the per-chunk launch cost (four launches) is noise against
 // the ~19 ms of encoder work in a full chunk.
 constexpr size_t kChunk = size_t(1) << 24;
-constexpr bool kPairs = LZ4R_PAIRS != 0;
 static_assert(kChunk % kPart == 0, "chunks start on a scan partial");
 static_assert((kChunk / 8) * 8 * 64 < (size_t(1) << 32), "chunk grid fits HIP's limit");
 // largest input one call accepts (block indices are u32 in the per-call arrays)
@@ -1892,25 +1448,9 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
     if (timed) (void)hipEventRecord(c->ev_tiles[2 * k], s);
     // (every chunk starts 300 b0 bytes in: a multiple of 4)
     if (((uintptr_t)in & 3) == 0) {
-      // pairs of full blocks (lz4_pairs: two blocks per wave), then the last
-      // one or two blocks of the chunk, one per wave (lz4_tiles); a pair's
-      // second block is never the chunk's last (its 4-grams read 24 bytes on)
-      // (B's row 4 reads 24 bytes into the block after it: with a last block
-      // of < 24 bytes the pair before it stays with lz4_tiles)
-      const size_t npairs = kPairs && nbc >= 2 ? (last_n >= 24 ? nbc - 1 : nbc - 2) / 2 : 0;
-#if LZ4R_PAIRS
-      if (npairs) {
-        const uint32_t pper = (uint32_t)((npairs + 7) / 8);
-        hipLaunchKernelGGL(lz4_pairs, dim3(8 * pper), dim3(64), 0, s, in + b0 * kBlk,
-                           (uint32_t)npairs, pper, c->slots, c->tsz + b0, c->bsizes + b0,
-                           c->status);
-      }
-#endif
-      const size_t t0 = 2 * npairs, nrest = nbc - t0;
-      const uint32_t rper = (uint32_t)((nrest + 7) / 8);
-      hipLaunchKernelGGL(lz4_tiles<true>, dim3(8 * rper), dim3(64), 0, s,
-                         in + (b0 + t0) * kBlk, (uint32_t)nrest, rper, last_n,
-                         c->slots + t0 * kSlot, c->tsz + b0 + t0, c->bsizes + b0 + t0, c->status);
+      hipLaunchKernelGGL(lz4_tiles<true>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
+                         (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0,
+                         c->status);
     } else
       hipLaunchKernelGGL(lz4_tiles<false>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
                          (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0,

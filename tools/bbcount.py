@@ -81,18 +81,19 @@ def basic_blocks(L, st, en):
     return bbs
 
 
-BUMP = ["\ts_mov_b64 s[80:81], exec",
+# (registers {v}, {v1}, {v2} and s[{s}:{s1}] above every one the kernel uses)
+BUMP = ["\ts_mov_b64 s[{s}:{s1}], exec",
         "\ts_mov_b64 exec, 1",
         "\ts_nop 1",
-        "\tglobal_atomic_add v[60:61], v62, off offset:{off}",
-        "\ts_mov_b64 exec, s[80:81]",
+        "\tglobal_atomic_add v[{v}:{v1}], v{v2}, off offset:{off}",
+        "\ts_mov_b64 exec, s[{s}:{s1}]",
         "\ts_nop 1"]
-PROLOGUE = ["\ts_getpc_b64 s[80:81]",
-            "\ts_add_u32 s80, s80, lz4r_bb_acc@rel32@lo+4",
-            "\ts_addc_u32 s81, s81, lz4r_bb_acc@rel32@hi+12",
-            "\tv_mov_b32 v60, s80",
-            "\tv_mov_b32 v61, s81",
-            "\tv_mov_b32 v62, 1"]
+PROLOGUE = ["\ts_getpc_b64 s[{s}:{s1}]",
+            "\ts_add_u32 s{s}, s{s}, lz4r_bb_acc@rel32@lo+4",
+            "\ts_addc_u32 s{s1}, s{s1}, lz4r_bb_acc@rel32@hi+12",
+            "\tv_mov_b32 v{v}, s{s}",
+            "\tv_mov_b32 v{v1}, s{s1}",
+            "\tv_mov_b32 v{v2}, 1"]
 
 
 def instrument(L, st, en):
@@ -108,28 +109,30 @@ def instrument(L, st, en):
             used.update(("s", k) for k in range(int(a), int(b) + 1))
         for r in re.findall(r"\bs(\d+)\b", t):
             used.add(("s", int(r)))
-    assert max(k for t, k in used if t == "v") < 60, "v60.. in use"
-    assert max(k for t, k in used if t == "s") < 80, "s80.. in use"
-    out = list(L[:st + 1]) + PROLOGUE
+    vb = (max(k for t, k in used if t == "v") + 2) & ~1
+    sb = (max(k for t, k in used if t == "s") + 2) & ~1
+    R = dict(v=vb, v1=vb + 1, v2=vb + 2, s=sb, s1=sb + 1)
+    assert vb + 3 <= 256 and sb + 2 <= 100
+    out = list(L[:st + 1]) + [x.format(**R) for x in PROLOGUE]
     k = 0
     off = lambda k: f"{4 * k}"
-    out += [b.format(off=off(k)) for b in BUMP]      # entry block
+    out += [b.format(off=off(k), **R) for b in BUMP]      # entry block
     k += 1
     for i in range(st + 1, en):
         out.append(L[i])
         if LABEL.match(L[i]):
-            out += [b.format(off=off(k)) for b in BUMP]
+            out += [b.format(off=off(k), **R) for b in BUMP]
             k += 1
     assert k <= NCNT and 4 * k < 4096
     out += L[en:]
     txt = "\n".join(out)
     # descriptor / metadata: cover v60..v62 and s80..s81
     txt = re.sub(r"(\.amdhsa_kernel " + KERNEL + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_vgpr )\d+",
-                 r"\g<1>64", txt)
+                 rf"\g<1>{(vb + 4 + 3) & ~3}", txt)
     txt = re.sub(r"(\.amdhsa_kernel " + KERNEL + r"\n(?:.*\n)*?\s*\.amdhsa_accum_offset )\d+",
-                 r"\g<1>64", txt)
+                 rf"\g<1>{(vb + 4 + 3) & ~3}", txt)
     txt = re.sub(r"(\.amdhsa_kernel " + KERNEL + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_sgpr )\d+",
-                 r"\g<1>84", txt)
+                 rf"\g<1>{sb + 2}", txt)
     txt += ("\n\t.type\tlz4r_bb_acc,@object\n\t.section\t.bss.lz4r_bb_acc,\"aw\",@nobits\n"
             "\t.globl\tlz4r_bb_acc\n\t.protected\tlz4r_bb_acc\n\t.p2align\t8\nlz4r_bb_acc:\n\t.zero\t4096\n"
             "\t.size\tlz4r_bb_acc, 4096\n")
@@ -210,7 +213,7 @@ def run(outdir, name="prod", nbytes=1 << 30):
 
 # cycles per wave-instruction per SIMD at 8 waves per SIMD (tools/valu_rate.hip;
 # profiles/r03_valu_rate.log, profiles/r05_valu_rate.log)
-FAST = {"v_add_u32", "v_xor_b32", "v_and_b32", "v_or_b32"}
+FAST = {"v_add_u32", "v_xor_b32", "v_and_b32", "v_or_b32", "v_sub_u32", "v_mov_b32"}
 
 
 def vcost(ins, table):
@@ -218,7 +221,7 @@ def vcost(ins, table):
     base = re.sub(r"_e(32|64)$", "", op)
     args = ins.split(None, 1)[1] if " " in ins else ""
     srcs = ",".join(args.split(",")[1:])
-    sgpr_src = bool(re.search(r"\bs\[?\d", srcs)) or "exec" in srcs
+    sgpr_src = bool(re.search(r"\bs\[?\d|\bvcc_(lo|hi)\b|\bexec|\bm0\b", srcs))
     if "_dpp" in op or " row_" in ins or "wave_sh" in ins or "quad_perm" in ins:
         return table["dpp"]
     if base in FAST:
@@ -226,10 +229,10 @@ def vcost(ins, table):
     for k in ("v_lshlrev_b64", "v_lshrrev_b64", "v_ashrrev_i64"):
         if base == k:
             return table["shift64"]
+    if base == "v_cndmask_b32" and op.endswith("_e32"):
+        return table["v_cndmask_b32_e32_vcc"]
     if base in table:
         return table[base]
-    if base == "v_cndmask_b32" and op.endswith("_e32"):
-        return table["v_cndmask_b32_e32_vcc_valu"]
     return table["default"]
 
 
