@@ -330,6 +330,51 @@ __global__ __launch_bounds__(64) void body(uint32_t *out, uint64_t *clk) {
           "v_and_b32_e32 %0, %5, %0\n\tv_and_b32_e32 %1, %4, %1\n\t"
           "v_and_b32_e32 %2, %5, %2\n\tv_and_b32_e32 %3, %4, %3\n\t"
           : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "s"(s0), "s"(s1));
+    } else if (KIND == 43) { // 4 v_perm_b32 + 4 v_add_u32 interleaved (is the cost additive?)
+      asm volatile(
+          "v_perm_b32 %0, %1, %0, %4\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_perm_b32 %2, %3, %2, %4\n\tv_add_u32 %3, %3, %0\n\t"
+          "v_perm_b32 %0, %1, %0, %4\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_perm_b32 %2, %3, %2, %4\n\tv_add_u32 %3, %3, %0\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "s"(0x05040100u));
+    } else if (KIND == 44) { // 4 v_cndmask_b32_e64 + 4 v_add_u32 interleaved
+      asm volatile(
+          "v_cndmask_b32_e64 %0, %0, %1, %4\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_cndmask_b32_e64 %2, %2, %3, %5\n\tv_add_u32 %3, %3, %0\n\t"
+          "v_cndmask_b32_e64 %0, %0, %1, %5\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_cndmask_b32_e64 %2, %2, %3, %4\n\tv_add_u32 %3, %3, %0\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d)
+          : "s"((uint64_t)s0 * 0x9E3779B97F4A7C15ull), "s"((uint64_t)s1 * 0xC2B2AE3D27D4EB4Full));
+    } else if (KIND == 45) { // 4 v_max_u32_dpp + 4 v_add_u32 interleaved
+      asm volatile(
+          "v_max_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_max_u32_dpp %2, %2, %2 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\tv_add_u32 %3, %3, %0\n\t"
+          "v_max_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_max_u32_dpp %2, %2, %2 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\tv_add_u32 %3, %3, %0\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 46) { // 4 v_lshrrev_b32 + 4 v_add_u32 interleaved
+      asm volatile(
+          "v_lshrrev_b32 %0, 3, %0\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_lshrrev_b32 %2, 5, %2\n\tv_add_u32 %3, %3, %0\n\t"
+          "v_lshrrev_b32 %0, 7, %0\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_lshrrev_b32 %2, 2, %2\n\tv_add_u32 %3, %3, %0\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    } else if (KIND == 47) { // 4 v_perm_b32 + 4 v_cndmask_b32_e64 interleaved (two slow classes)
+      asm volatile(
+          "v_perm_b32 %0, %1, %0, %6\n\tv_cndmask_b32_e64 %1, %1, %2, %4\n\t"
+          "v_perm_b32 %2, %3, %2, %6\n\tv_cndmask_b32_e64 %3, %3, %0, %5\n\t"
+          "v_perm_b32 %0, %1, %0, %6\n\tv_cndmask_b32_e64 %1, %1, %2, %5\n\t"
+          "v_perm_b32 %2, %3, %2, %6\n\tv_cndmask_b32_e64 %3, %3, %0, %4\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d)
+          : "s"((uint64_t)s0 * 0x9E3779B97F4A7C15ull), "s"((uint64_t)s1 * 0xC2B2AE3D27D4EB4Full),
+            "s"(0x05040100u));
+    } else if (KIND == 48) { // 4 v_perm_b32 + 4 s_add (slow VALU beside SALU)
+      asm volatile(
+          "v_perm_b32 %0, %1, %0, %6\n\ts_add_u32 %4, %4, %5\n\t"
+          "v_perm_b32 %2, %3, %2, %6\n\ts_add_u32 %5, %5, %4\n\t"
+          "v_perm_b32 %0, %1, %0, %6\n\ts_xor_b32 %4, %4, %5\n\t"
+          "v_perm_b32 %2, %3, %2, %6\n\ts_xor_b32 %5, %5, %4\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "+s"(s1) : "s"(0x05040100u) : "scc");
     } else {                 // 4 VALU + 4 SALU interleaved
       asm volatile(
           "v_add_u32 %0, %0, %1\n\ts_add_u32 %4, %4, %5\n\tv_add_u32 %1, %1, %2\n\t"
@@ -420,5 +465,11 @@ int main() {
   run<40>("v_mov_b32 from sgpr", grid, out, clk);
   run<41>("v_lshl_or/add_lshl/lshl_add", grid, out, clk);
   run<42>("v_and_b32 sgpr (vop2)", grid, out, clk);
+  run<43>("4 v_perm + 4 v_add", grid, out, clk);
+  run<44>("4 v_cndmask + 4 v_add", grid, out, clk);
+  run<45>("4 dpp + 4 v_add", grid, out, clk);
+  run<46>("4 v_lshrrev + 4 v_add", grid, out, clk);
+  run<47>("4 v_perm + 4 v_cndmask", grid, out, clk);
+  run<48>("4 v_perm + 4 s_add", grid, out, clk);
   return 0;
 }
