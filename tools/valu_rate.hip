@@ -375,6 +375,145 @@ __global__ __launch_bounds__(64) void body(uint32_t *out, uint64_t *clk) {
           "v_perm_b32 %0, %1, %0, %6\n\ts_xor_b32 %4, %4, %5\n\t"
           "v_perm_b32 %2, %3, %2, %6\n\ts_xor_b32 %5, %5, %4\n\t"
           : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "+s"(s1) : "s"(0x05040100u) : "scc");
+    } else if (KIND == 50) { // 4 v_mbcnt + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_mbcnt_lo_u32_b32 %0, %4, %0\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_mbcnt_hi_u32_b32 %2, %4, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_mbcnt_lo_u32_b32 %0, %4, %0\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_mbcnt_hi_u32_b32 %2, %4, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 51) { // 4 v_readlane + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_readlane_b32 %5, %0, 63\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_readfirstlane_b32 %5, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_readlane_b32 %5, %0, 63\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_readfirstlane_b32 %5, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 52) { // 4 v_writelane + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_writelane_b32 %0, %4, 5\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_writelane_b32 %2, %4, 9\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_writelane_b32 %0, %4, 5\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_writelane_b32 %2, %4, 9\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 53) { // 4 v_alignbyte + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_alignbyte_b32 %0, %1, %0, %3\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_alignbyte_b32 %2, %3, %2, %1\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_alignbyte_b32 %0, %1, %0, %3\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_alignbyte_b32 %2, %3, %2, %1\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 54) { // 4 v_mul_lo_u32 + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_mul_lo_u32 %0, %0, %1\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_mul_lo_u32 %2, %2, %3\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_mul_lo_u32 %0, %0, %1\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_mul_lo_u32 %2, %2, %3\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 55) { // 4 v_bfe/bfi + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_bfe_u32 %0, %1, 3, 9\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_bfi_b32 %2, %3, %1, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_bfe_u32 %0, %1, 3, 9\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_bfi_b32 %2, %3, %1, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 56) { // 4 v_add3/lshl_add + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_add3_u32 %0, %0, %1, %3\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_lshl_add_u32 %2, %3, 2, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_add3_u32 %0, %0, %1, %3\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_lshl_add_u32 %2, %3, 2, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 57) { // 4 v_cmp_e64 + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_cmp_lt_u32_e64 %6, %0, %1\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_cmp_lt_u32_e64 %6, %2, %3\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_cmp_lt_u32_e64 %6, %0, %1\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_cmp_lt_u32_e64 %6, %2, %3\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 58) { // 4 v_ffbl + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_ffbl_b32_e32 %0, %1\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_ffbl_b32_e32 %2, %3\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_ffbl_b32_e32 %0, %1\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_ffbl_b32_e32 %2, %3\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 59) { // 4 v_max/min + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_max_u32_e32 %0, %0, %1\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_min_u32_e32 %2, %2, %3\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_max_u32_e32 %0, %0, %1\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_min_u32_e32 %2, %2, %3\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 60) { // 4 v_lshl_add_u64 + 4 v_add_u32 interleaved
+      uint64_t x = ((uint64_t)a << 32) | b;
+      asm volatile(
+          "v_lshl_add_u64 %0, %0, 2, %0\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_lshl_add_u64 %0, %0, 1, %0\n\tv_add_u32 %2, %2, %1\n\t"
+          "v_lshl_add_u64 %0, %0, 2, %0\n\tv_add_u32 %1, %1, %2\n\t"
+          "v_lshl_add_u64 %0, %0, 1, %0\n\tv_add_u32 %2, %2, %1\n\t"
+          : "+v"(x), "+v"(c), "+v"(d));
+      a = (uint32_t)x; b = (uint32_t)(x >> 32);
+    } else if (KIND == 61) { // 4 v_add sgpr + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_add_u32_e32 %0, %4, %0\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_and_b32_e32 %2, %4, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_add_u32_e32 %0, %4, %0\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_and_b32_e32 %2, %4, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 62) { // 4 v_mov from sgpr + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_mov_b32_e32 %0, %4\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_mov_b32_e32 %2, %4\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_mov_b32_e32 %0, %4\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_mov_b32_e32 %2, %4\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
+    } else if (KIND == 63) { // 4 v_perm/xad + 4 v_add_u32 interleaved
+      uint32_t t5 = 0;
+      uint64_t m6 = 0;
+      asm volatile(
+          "v_xad_u32 %0, %1, %3, %0\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_and_or_b32 %2, %3, %1, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          "v_xad_u32 %0, %1, %3, %0\n\tv_add_u32 %1, %1, %3\n\t"
+          "v_and_or_b32 %2, %3, %1, %2\n\tv_add_u32 %3, %3, %1\n\t"
+          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+s"(s0), "=&s"(t5), "=&s"(m6));
+      s1 ^= t5 ^ (uint32_t)m6;
     } else {                 // 4 VALU + 4 SALU interleaved
       asm volatile(
           "v_add_u32 %0, %0, %1\n\ts_add_u32 %4, %4, %5\n\tv_add_u32 %1, %1, %2\n\t"
@@ -471,5 +610,19 @@ int main() {
   run<46>("4 v_lshrrev + 4 v_add", grid, out, clk);
   run<47>("4 v_perm + 4 v_cndmask", grid, out, clk);
   run<48>("4 v_perm + 4 s_add", grid, out, clk);
+  run<50>("4 v_mbcnt + 4 v_add", grid, out, clk);
+  run<51>("4 v_readlane + 4 v_add", grid, out, clk);
+  run<52>("4 v_writelane + 4 v_add", grid, out, clk);
+  run<53>("4 v_alignbyte + 4 v_add", grid, out, clk);
+  run<54>("4 v_mul_lo_u32 + 4 v_add", grid, out, clk);
+  run<55>("4 v_bfe/bfi + 4 v_add", grid, out, clk);
+  run<56>("4 v_add3/lshl_add + 4 v_add", grid, out, clk);
+  run<57>("4 v_cmp_e64 + 4 v_add", grid, out, clk);
+  run<58>("4 v_ffbl + 4 v_add", grid, out, clk);
+  run<59>("4 v_max/min + 4 v_add", grid, out, clk);
+  run<60>("4 v_lshl_add_u64 + 4 v_add", grid, out, clk);
+  run<61>("4 v_add sgpr + 4 v_add", grid, out, clk);
+  run<62>("4 v_mov from sgpr + 4 v_add", grid, out, clk);
+  run<63>("4 v_perm/xad + 4 v_add", grid, out, clk);
   return 0;
 }
