@@ -40,9 +40,9 @@ FP64_VALU_PEAK_TOPS = 39.3     # 78.6 TFLOPS fp64 vector spec counts FMA as 2
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # (tools/traffic.sh -> tools/traffic_summary.py, gfx950 FETCH correction applied)
 TRAFFIC_JSON = os.path.join(REPO, "profiles", "r04_traffic.json")
-# per-launch instruction counts of lz4_tiles + measured SIMD issue rates
-# (tools/issue.sh -> tools/issue_summary.py)
-ISSUE_JSON = os.path.join(REPO, "profiles", "r04_issue.json")
+# lz4_tiles' per-pipe roof from one profiled run (tools/r05_roof.sh ->
+# tools/roof.py): dynamic opcode counts, PMC counts, time and clock together
+ROOF_JSON = os.path.join(REPO, "profiles", "r05_roof.json")
 # clock each kernel holds under its own load (DVFS give-back), from a
 # GRBM_GUI_ACTIVE PMC pass (tools/clock_pmc.sh -> tools/clock_summary.py)
 CLOCK_JSON = os.path.join(REPO, "profiles", "r04_clock.json")
@@ -59,8 +59,9 @@ def log(*a):
 
 def _profile_json(path):
     """This round's profile, else the latest earlier round's."""
-    for r in ("r04_", "r03_", "r02_", "r01_"):
-        p = path.replace("r04_", r)
+    base = os.path.basename(path)[:4]
+    for r in ("r05_", "r04_", "r03_", "r02_", "r01_"):
+        p = path.replace(base, r)
         if os.path.exists(p):
             return p
     return path
@@ -112,54 +113,39 @@ def at_held_clock(achieved, peak_spec, key):
 
 
 def issue_roof(bytes_now, launch_ms):
-    """The compressor's binding roof: wave-instruction issue.  Counts per
-    launch from PMC (scaled to this input), rates from the micro-benchmark."""
+    """lz4_tiles' binding roof (tools/roof.py -> ROOF_JSON): per 300-B block,
+    lower bounds on the SIMD cycles of its VALU instructions (the dynamic
+    opcode counts of tools/bbcount.py priced at the cheapest issue rate the
+    micro-benchmarks measure for each class), its SALU instructions and its
+    LDS-array cycles, all from one profiled run on one box (counts, time and
+    clock of the same dispatches).  frac = the largest pipe's CU cycles per
+    block / the measured CU cycles per block of that run (<= 1: lower
+    bounds); frac_live prices this bench's own lz4_tiles time at the
+    profile's clock."""
     try:
-        d = json.load(open(_profile_json(ISSUE_JSON)))
-        pl, rates = d["lz4"]["per_launch"], d["issue_rates_winstr_per_s"]
-        scale = bytes_now / d["lz4"]["bytes_per_launch"]
-        valu = pl["SQ_INSTS_VALU"] * scale
-        salu = pl["SQ_INSTS_SALU"] * scale
-        peak_mix = rates["4 valu + 4 salu"]
-        peak_valu = rates["v_add/xor/and/or"]
-    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        d = json.load(open(_profile_json(ROOF_JSON)))
+        roof = d["roof_cu_cycles_per_block"]
+        bind = d["binding_pipe"]
+        meas = d["measured"]["median"]
+    except (OSError, KeyError, ValueError):
         return None
-    sec = launch_ms / 1e3
-    # the micro-benchmark's rate was measured at the clock it held (valu_rate's
-    # v_add body); per cycle, the kernel's own clock sets its peak
-    clk = {}
-    # (lz4_tiles is a template since round 3: its clock key names the instance)
-    fk = held_clock("lz4:void lz4_tiles<true>") or held_clock("lz4:lz4_tiles")
-    fb = held_clock("valu:void body<0>")
-    fm = held_clock("valu:void body<3>")               # the 4 VALU + 4 SALU body
-    if fk and fb:
-        pk = peak_valu * fk / fb
-        clk = {"held_clock_ghz": fk, "bench_clock_ghz": fb,
-               "peak_at_held_clock": round(pk / 1e9, 1),
-               "frac_at_held_clock": round(valu / sec / pk, 4)}
-        if fm:
-            pm = peak_mix * fk / fm
-            clk["mixed_stream_peak_at_held_clock"] = round(pm / 1e9, 1)
-            clk["valu_salu_frac_at_held_clock"] = round((valu + salu) / sec / pm, 4)
+    nb = (bytes_now + 299) // 300
+    live_cyc = launch_ms / 1e3 * meas["clock_ghz"] * 1e9 * 256 / nb
     return {
-        **clk,
-        "bound": "issue (VALU + SALU wave-instructions)", "unit": "Gwinstr/s",
-        "achieved": round(valu / sec / 1e9, 1), "peak": round(peak_valu / 1e9, 1),
-        "frac": round(valu / sec / peak_valu, 4),
-        "valu_salu_gwinstr_s": round((valu + salu) / sec / 1e9, 1),
-        "mixed_stream_peak": round(peak_mix / 1e9, 1),
-        "per_block": {"valu": round(pl["SQ_INSTS_VALU"] / pl["SQ_WAVES"], 1),
-                      "salu": round(pl["SQ_INSTS_SALU"] / pl["SQ_WAVES"], 1),
-                      "lds": round(pl["SQ_INSTS_LDS"] / pl["SQ_WAVES"], 1),
-                      "branch": round(pl["SQ_INSTS_BRANCH"] / pl["SQ_WAVES"], 1)},
-        "note": "achieved = PMC SQ_INSTS_VALU per launch (" +
-                os.path.basename(_profile_json(ISSUE_JSON)) + ", scaled to this input) / "
-                "lz4_tiles time; peak = the chip's measured v_add/xor/and/or rate at 8 waves "
-                "per SIMD (tools/valu_rate.hip).  At the clocks each holds under load "
-                "(" + os.path.basename(CLOCK_JSON) + ": the micro-benchmark bodies run slower "
-                "than lz4_tiles) the kernel's VALU + SALU issue runs at "
-                "valu_salu_frac_at_held_clock of an interleaved 4 VALU + 4 SALU stream: "
-                "VALU and SALU instructions together are the binding issue roof",
+        "bound": f"{bind} issue", "unit": "CU cycles per 300-B block",
+        "roof_cu_cycles_per_block": roof, "binding_pipe": bind,
+        "measured_cu_cycles_per_block": meas["cu_cycles_per_block"],
+        "profile_clock_ghz": meas["clock_ghz"], "profile_ms": meas["ms"],
+        "frac": d["frac"], "frac_by_pipe": d["frac_by_pipe"],
+        "live_cu_cycles_per_block_at_profile_clock": round(live_cyc, 1),
+        "frac_live": round(roof[bind] / live_cyc, 4),
+        "per_block": d["per_block"],
+        "note": "from " + os.path.basename(_profile_json(ROOF_JSON)) + " (tools/roof.py): "
+                "VALU = lower bound of the vector-issue cycles per block per SIMD "
+                "(per-opcode dynamic counts x the cheapest measured rate of each class, "
+                "tools/valu_rate.hip), SALU = SQ_INSTS_SALU x the s_add rate, LDS = "
+                "SQ_LDS_IDX_ACTIVE; four SIMDs share a CU's LDS, so the roof is "
+                "max(VALU/4, SALU/4, LDS) CU cycles per block",
     }
 
 
