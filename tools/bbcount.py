@@ -33,7 +33,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "tools", "ab")
 LLVM = "/opt/rocm/lib/llvm/bin"
-KERNEL = "_ZN12_GLOBAL__N_19lz4_tilesILb1EEEvPKhjjjPhPjPtS4_"
+KERNEL = "_ZN12_GLOBAL__N_19lz4_tilesILb1EE"      # (a prefix: signatures change)
 NCNT = 1024
 LABEL = re.compile(r"^(\.LBB\d+_\d+):|^; (%bb\.\d+):|^\s*(1):\s*$")
 
@@ -53,7 +53,7 @@ def compile_asm(src, extra=()):
 
 
 def kernel_range(L, name=KERNEL):
-    st = next(i for i, l in enumerate(L) if l.startswith(name + ":"))
+    st = next(i for i, l in enumerate(L) if l.startswith(name) and l.split(":")[0].endswith("_"))
     en = next(i for i in range(st, len(L)) if L[i].startswith(".Lfunc_end"))
     return st, en
 
@@ -96,7 +96,7 @@ PROLOGUE = ["\ts_getpc_b64 s[{s}:{s1}]",
             "\tv_mov_b32 v{v2}, 1"]
 
 
-def instrument(L, st, en):
+def instrument(L, st, en, kname):
     body = L[st:en]
     used = set()
     for l in body:
@@ -127,11 +127,11 @@ def instrument(L, st, en):
     out += L[en:]
     txt = "\n".join(out)
     # descriptor / metadata: cover v60..v62 and s80..s81
-    txt = re.sub(r"(\.amdhsa_kernel " + KERNEL + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_vgpr )\d+",
+    txt = re.sub(r"(\.amdhsa_kernel " + kname + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_vgpr )\d+",
                  rf"\g<1>{(vb + 4 + 3) & ~3}", txt)
-    txt = re.sub(r"(\.amdhsa_kernel " + KERNEL + r"\n(?:.*\n)*?\s*\.amdhsa_accum_offset )\d+",
+    txt = re.sub(r"(\.amdhsa_kernel " + kname + r"\n(?:.*\n)*?\s*\.amdhsa_accum_offset )\d+",
                  rf"\g<1>{(vb + 4 + 3) & ~3}", txt)
-    txt = re.sub(r"(\.amdhsa_kernel " + KERNEL + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_sgpr )\d+",
+    txt = re.sub(r"(\.amdhsa_kernel " + kname + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_sgpr )\d+",
                  rf"\g<1>{sb + 2}", txt)
     txt += ("\n\t.type\tlz4r_bb_acc,@object\n\t.section\t.bss.lz4r_bb_acc,\"aw\",@nobits\n"
             "\t.globl\tlz4r_bb_acc\n\t.protected\tlz4r_bb_acc\n\t.p2align\t8\nlz4r_bb_acc:\n\t.zero\t4096\n"
@@ -144,7 +144,8 @@ def build(src=None, name="prod"):
     L = compile_asm(src)
     st, en = kernel_range(L)
     bbs = basic_blocks(L, st, en)
-    txt, k = instrument(L, st, en)
+    kname = L[st].split(":")[0]
+    txt, k = instrument(L, st, en, kname)
     assert k == len(bbs), (k, len(bbs))
     s = os.path.join(OUT, f"bbcnt_{name}.s")
     open(s, "w").write(txt)
@@ -153,7 +154,7 @@ def build(src=None, name="prod"):
                     "-o", o], check=True)
     subprocess.run([f"{LLVM}/ld.lld", "-shared", o, "-o", os.path.join(OUT, f"bbcnt_{name}.co")],
                    check=True)
-    json.dump({"kernel": KERNEL, "bbs": bbs},
+    json.dump({"kernel": kname, "bbs": bbs},
               open(os.path.join(OUT, f"bb_static_{name}.json"), "w"))
     print(f"{len(bbs)} basic blocks, {sum(len(b) for _, b in bbs)} static instructions")
 
@@ -180,16 +181,19 @@ def run(outdir, name="prod", nbytes=1 << 30):
     assert hip.hipModuleLoad(ctypes.byref(mod),
                              os.path.join(OUT, f"bbcnt_{name}.co").encode()) == 0
     fn = ctypes.c_void_p()
-    assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, KERNEL.encode()) == 0
+    kname = json.load(open(os.path.join(OUT, f"bb_static_{name}.json")))["kernel"]
+    assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, kname.encode()) == 0
     acc, accsz = ctypes.c_void_p(), ctypes.c_size_t()
     assert hip.hipModuleGetGlobal(ctypes.byref(acc), ctypes.byref(accsz), mod,
                                   b"lz4r_bb_acc") == 0
     assert hip.hipMemset(acc, 0, ctypes.c_size_t(4 * NCNT)) == 0
     per = (nb + 7) // 8
     args = [ctypes.c_void_p(d_in.data_ptr()), ctypes.c_uint32(nb), ctypes.c_uint32(per),
-            ctypes.c_uint32(last_n), ctypes.c_void_p(slots.data_ptr()),
-            ctypes.c_void_p(usz.data_ptr()), ctypes.c_void_p(bsz.data_ptr()),
-            ctypes.c_void_p(status.data_ptr())]
+            ctypes.c_uint32(last_n), ctypes.c_void_p(slots.data_ptr())]
+    if "jjjPhS" in kname:             # (heads, overflow slots) since round 5
+        args.append(ctypes.c_void_p(slots.data_ptr() + nb * 96))
+    args += [ctypes.c_void_p(usz.data_ptr()), ctypes.c_void_p(bsz.data_ptr()),
+             ctypes.c_void_p(status.data_ptr())]
     params = (ctypes.c_void_p * len(args))(*[ctypes.cast(ctypes.pointer(a), ctypes.c_void_p)
                                               for a in args])
     assert hip.hipModuleLaunchKernel(fn, 8 * per, 1, 1, 64, 1, 1, 0, None, params, None) == 0

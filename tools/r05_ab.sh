@@ -15,6 +15,14 @@ for v in prod "$@"; do
 done
 AB_NOPMC=1 bash tools/ab4.sh "$@"
 rc=$?
+if [ $rc = 0 ] && [ -n "$AB_FETCH" ]; then
+  # FETCH_SIZE (KiB, x2 for 16-B streaming reads) of the compressor kernels per variant
+  for v in prod "$@"; do
+    lib=""; [ $v = prod ] || lib=$PWD/tools/ab/liblz4_$v.so
+    LZ4JPEG_LIB=$lib timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/f_$v -o run -- python3 tools/lz4_one.py 1073741824 2 1 > $O/f_$v.log 2>&1 || { echo "fetch $v failed"; rc=1; break; }
+    echo "== fetch $v"; python3 tools/pmc_summary.py $O/f_$v/run_results.db lz4_ | grep -E "dispatch|FETCH" | tail -4
+  done
+fi
 tail -20 $O/valu_rate.log 2>/dev/null
 cat $O/bbcount_*.log
 exit $rc
