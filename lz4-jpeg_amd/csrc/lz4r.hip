@@ -46,7 +46,9 @@
 //            takes and of its size fields; record k = the sequence's match
 //            word dist | M << 9 | (match start + M) << 19 (its literal run
 //            starts where sequence k - 1's match ends; the literal tail is
-//            n << 19) -> the block's slot, after a header dword (sum of the size
+//            n << 19) -> the block's record scratch (a dense 96-B head: header
+//            and records 0..22; an overflow slot for the rest), after a header
+//            dword (sum of the size
 //            fields | sequence count << 16); the block's byte count -> usz
 //            (u32, for the scan) and bsizes (u16).
 // lz4_scan_reduce / lz4_scan_partials: exclusive scan of the block sizes.
@@ -66,7 +68,7 @@
 // heads, staged input) before waiting on any: one memory round trip per
 // workgroup instead of three (0.91 -> 0.75 ms per GiB).
 // HBM traffic per input byte: 1 B read + ~0.35 B of records written by
-// lz4_tiles; ~1 B of input + ~0.43 B of record heads read and ~1.03 B
+// lz4_tiles; ~1 B of input + ~0.33 B of record heads read and ~1.03 B
 // written by lz4_emit (+14 B/block of sizes and offsets).
 #include <hip/hip_runtime.h>
 #include <limits.h>
@@ -149,12 +151,18 @@ static_assert(kInOff + kBlk + 48 <= kQOff && kQOff % 16 == 0 && kInOff % 16 == 0
                   kBlk == 75 * 4,
               "dword staging (75 dwords), aligned regions");
 
-// scratch bytes per block slot: the header dword and <= 121 sequence records;
-// 5 x 128 B, so a block's record head (the 128 B lz4_emit stages) is one L2
-// line, not two (560-B slots straddled a line boundary 7 times in 8)
-constexpr int kSlot = 640;
-static_assert(kSlot % 16 == 0 && kSlot >= kBlkOutMax && kBlkOutMax / 16 <= 64,
-              "aligned slots, one store round");
+// Record scratch per block: the header dword and <= 121 sequence records.
+// The first kHeadW dwords (header + 23 records: all of a text block's but for
+// ~7 % of blocks) go to a dense head array, kHead bytes per block, so lz4_emit
+// reads its 32 blocks' heads as one contiguous 3 KB run of 16-B loads (no
+// 128-B line per block of which ~60 B were used); records 23.. go to a
+// per-block overflow slot of kOvf bytes.
+constexpr int kHeadW = 24;
+constexpr int kHead = 4 * kHeadW;        // 96 B
+constexpr int kOvf = 400;                // records 23..120: <= 98 dwords
+constexpr int kSlot = kHead + kOvf;      // scratch bytes per block
+static_assert(kHead % 16 == 0 && kOvf % 16 == 0 && 4 * (121 + 1 - kHeadW) <= kOvf,
+              "aligned head and overflow slots");
 
 struct TileLds {
   alignas(16) uint8_t buf[kBufBytes];
@@ -420,14 +428,16 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("" ::: "memory");
 }
 
-// Encode the staged block (n bytes at S.buf[kInOff]) as sequence records at
-// recs (global: the block's slot); returns the bytes its stream takes.
+// Encode the staged block (n bytes at S.buf[kInOff]) as sequence records:
+// dwords 0 .. kHeadW - 1 (header, records 0..22) at head, record k >= 23 at
+// ovf[k + 1 - kHeadW]; returns the bytes its stream takes.
 // kMatchesOnly: stop after the best-match scan and store every position's
 // find_longest_match result to mout instead (lz4r_block_matches_device).
 template <bool kMatchesOnly, bool kFull>
 __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t *__restrict__ gsrc,
                                             uint32_t *__restrict__ mout,
-                                            uint32_t *__restrict__ recs,
+                                            uint32_t *__restrict__ head,
+                                            uint32_t *__restrict__ ovf,
                                             uint32_t *__restrict__ status) {
   // kFull: a whole 300-byte block of a 4-byte aligned input that is not the
   // launch's last (every block but one): n is a constant, only round 4's
@@ -812,7 +822,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
   // one round: sequence kk = s0 + lane has the match word wv (n << 19 -- no
   // match, M = dist = 0, ending at n -- past the matches); returns false once
   // the round holds the last sequence
-  auto round = [&](auto fast, int kk, uint32_t wv) {
+  auto round = [&](auto fast, int s0, uint32_t wv) {
+    const int kk = s0 + lane;
     const int M = (int)((wv >> 9) & 255u);
     const int end = (int)(wv >> 19);
     const uint32_t cq = (uint32_t)(end - M);                       // the match start
@@ -845,7 +856,16 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
       ocar += (int)(tot & 0xFFFFu);
       szsum += (int)(tot >> 16);
     }
-    store_lanes1(am, recs, 4u * (uint32_t)kk, wv);   // recs[1 + kk]: the sequence's word (the tail: n << 19)
+    // record dword 1 + kk (the sequence's word; the tail: n << 19): the head
+    // for kk < kHeadW - 1, the overflow slot after (the same lane offset off
+    // a base kHeadW dwords back)
+    if (s0 == 0) {
+      store_lanes1(am & ((1ull << (kHeadW - 1)) - 1), head, 4u * (uint32_t)kk, wv);
+      if (am >> (kHeadW - 1)) store_lanes1(am >> (kHeadW - 1) << (kHeadW - 1), ovf - kHeadW,
+                                           4u * (uint32_t)kk, wv);
+    } else {
+      store_lanes1(am, ovf - kHeadW, 4u * (uint32_t)kk, wv);
+    }
     nseq += (int)__popcll(am);
     return nm_r == 64;
   };
@@ -855,10 +875,10 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
     const uint32_t wtail = (uint32_t)n << 19;
     const uint32_t c0 = slow ? S.seq()[lane] : (lane < it ? seqv : wtail);
     auto rounds = [&](auto fast) {
-      if (round(fast, lane, c0)) {     // 64 match sequences: the tail or more follow
+      if (round(fast, 0, c0)) {        // 64 match sequences: the tail or more follow
         for (int s0 = 64;; s0 += 64) {
           const int kk = s0 + lane;
-          if (!round(fast, kk, slow && kk < Sv_slow ? S.seq()[kk] : wtail)) break;
+          if (!round(fast, s0, slow && kk < Sv_slow ? S.seq()[kk] : wtail)) break;
         }
       }
     };
@@ -868,15 +888,15 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
       rounds(std::false_type{});
   }
   PROF_MARK(6);                       // records
-  if (lane == 0) recs[0] = (uint32_t)szsum | ((uint32_t)nseq << 16);
+  if (lane == 0) head[0] = (uint32_t)szsum | ((uint32_t)nseq << 16);
   return ocar;
 }
 
 template <bool kAligned>   // the input is 4-byte aligned (the host checks)
 __global__ __launch_bounds__(64) void lz4_tiles(
     const uint8_t *__restrict__ in, uint32_t nb, uint32_t per, uint32_t last_n,
-    uint8_t *__restrict__ slots, uint32_t *__restrict__ usz, uint16_t *__restrict__ bsizes,
-    uint32_t *__restrict__ status) {
+    uint8_t *__restrict__ heads, uint8_t *__restrict__ ovfs, uint32_t *__restrict__ usz,
+    uint16_t *__restrict__ bsizes, uint32_t *__restrict__ status) {
   __shared__ TileLds S;
   const int lane = threadIdx.x;
   // XCD-aware order: workgroups w and w + 8 share an XCD (observed round-robin
@@ -888,7 +908,8 @@ __global__ __launch_bounds__(64) void lz4_tiles(
   const int n = t == nb - 1 ? (int)last_n : kBlk;
   const uint8_t *src = in + (size_t)t * kBlk;
 
-  uint32_t *const recs = reinterpret_cast<uint32_t *>(slots + (size_t)t * kSlot);
+  uint32_t *const head = reinterpret_cast<uint32_t *>(heads + (size_t)t * kHead);
+  uint32_t *const ovf = reinterpret_cast<uint32_t *>(ovfs + (size_t)t * kOvf);
   int W;
   if (kAligned && (t + 2 < nb || (t + 2 == nb && last_n >= 24))) {
     // no staging, the keys come straight from global memory
@@ -896,7 +917,7 @@ __global__ __launch_bounds__(64) void lz4_tiles(
     // (and a mid-walk lcp drain up to 15), so only where those bytes are the
     // launch's own -- every block but the last, and the one before it when
     // the last holds at least 24 bytes
-    W = encode_block<false, true>(S, kBlk, src, nullptr, recs, status);
+    W = encode_block<false, true>(S, kBlk, src, nullptr, head, ovf, status);
   } else {
     // the last block (n <= 300: nothing may be read past the input), the one
     // before a last block of < 24 bytes, or an unaligned input: staged
@@ -904,7 +925,7 @@ __global__ __launch_bounds__(64) void lz4_tiles(
     for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
     if (lane < 16) S.buf[kInOff + n + lane] = 0;
     wave_sync();
-    W = encode_block<false, false>(S, n, nullptr, nullptr, recs, status);
+    W = encode_block<false, false>(S, n, nullptr, nullptr, head, ovf, status);
   }
   if (lane == 0) {
     usz[t] = (uint32_t)W;
@@ -926,7 +947,7 @@ __global__ __launch_bounds__(64) void lz4_matches(const uint8_t *__restrict__ in
   for (int i = lane; i < n; i += 64) S.buf[kInOff + i] = src[i];
   if (lane < 16) S.buf[kInOff + n + lane] = 0;
   wave_sync();
-  encode_block<true, false>(S, n, nullptr, mout + (size_t)t * kBlk, nullptr, nullptr);
+  encode_block<true, false>(S, n, nullptr, mout + (size_t)t * kBlk, nullptr, nullptr, nullptr);
 }
 
 // find_longest_match over a block of any length n (block_encode with a
@@ -1081,7 +1102,7 @@ __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__
 // instruction issue as lz4_tiles is.
 constexpr int kGH = 32;                              // blocks per emit workgroup
 constexpr int kEW = 8;                               // waves per emit workgroup (4 blocks each)
-constexpr int kRecPre = 32;                          // record dwords per block staged in LDS
+constexpr int kRecPre = kHeadW;                      // record dwords per block staged in LDS
 constexpr int kGSplit = kGT / kGH;                   // workgroups per group
 constexpr int kEmitImg = kGH * kBlkOutMax + 32;      // worst case: every block 548 B
 constexpr int kStagePad = 16;                        // literal words reach 8 B before a run
@@ -1097,7 +1118,8 @@ __device__ __forceinline__ void or_bytes(uint32_t *buf32, int x, uint32_t v) {
 }
 
 __global__ __launch_bounds__(64 * kEW) void lz4_emit(
-    const uint8_t *__restrict__ in, const uint8_t *__restrict__ slots, size_t slot_base,
+    const uint8_t *__restrict__ in, const uint8_t *__restrict__ heads,
+    const uint8_t *__restrict__ ovfs, size_t slot_base,
     const uint32_t *__restrict__ tsz, size_t ntiles, size_t g_first,
     const uint32_t *__restrict__ gsum, const uint64_t *__restrict__ part,
     uint8_t *__restrict__ out, uint64_t cap, int hdr, uint64_t nb_total, uint32_t last_n,
@@ -1132,14 +1154,14 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
     pt = part[p];                                  // part[] holds absolute offsets
     tv = tid < nt ? tsz[g0 + tid] : 0u;
   }
-  constexpr int kPerSlot = kRecPre / 4;            // record heads: 32 slots x 128 B
+  constexpr int kPerSlot = kRecPre / 4;            // record heads: 32 x 96 B, contiguous
   static_assert(kGH * kPerSlot <= 64 * kEW, "one record load per thread");
   uint4 rv = make_uint4(0, 0, 0, 0);
   const int rhb = tid / kPerSlot, rj = tid % kPerSlot;
-  // the workgroup's slots: a uniform base and 32-bit offsets
-  const uint8_t *const wslots = slots + (b0 - slot_base) * (size_t)kSlot;
-  if (tid < (h1 - h0) * kPerSlot)
-    rv = reinterpret_cast<const uint4 *>(wslots + rhb * kSlot)[rj];
+  // the workgroup's heads (one contiguous run) and overflow slots
+  const uint8_t *const wheads = heads + (b0 - slot_base) * (size_t)kHead;
+  const uint8_t *const wovf = ovfs + (b0 - slot_base) * (size_t)kOvf;
+  if (tid < (h1 - h0) * kPerSlot) rv = reinterpret_cast<const uint4 *>(wheads)[tid];
   constexpr int kSt16 = (kGH * kBlk) / 16;         // 600 16-B chunks of staged input
   constexpr int kStPer = (kSt16 + 64 * kEW - 1) / (64 * kEW);
   uint4 sv[kStPer];
@@ -1217,8 +1239,9 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
         }
         const int k = f - sb;                      // sequence index in the block
         const int hb = bl0 + bi;
-        const uint32_t *rp = reinterpret_cast<const uint32_t *>(wslots + (hb - h0) * kSlot);
-        const uint32_t r = !valid ? 0u : (1 + k < kRecPre ? recst[hb - h0][1 + k] : rp[1 + k]);
+        const uint32_t *rp = reinterpret_cast<const uint32_t *>(wovf + (hb - h0) * kOvf);
+        const uint32_t r =
+            !valid ? 0u : (1 + k < kRecPre ? recst[hb - h0][1 + k] : rp[1 + k - kRecPre]);
         // record = the sequence's match word: dist | M << 9 | (match start +
         // M) << 19 (the literal tail: n << 19)
         const int M = (int)((r >> 9) & 255u), D = (int)(r & 511u);
@@ -1348,7 +1371,8 @@ struct lz4r_ctx {
   size_t cap_slots = 0;        // capacity of the slot scratch, in blocks (<= kChunk)
   uint16_t *bsizes = nullptr;  // encoded bytes of every block of the last call
   uint64_t *boff = nullptr;    // every block's offset from the first block byte
-  uint8_t *slots = nullptr;    // per-block record slots (kSlot bytes each), one chunk
+  uint8_t *slots = nullptr;    // per-block record scratch, one chunk: cap_slots heads of
+                               // kHead bytes, then cap_slots overflow slots of kOvf
   uint32_t *tsz = nullptr;     // encoded bytes per block (u32, for the scan)
   uint32_t *gsum = nullptr;    // encoded bytes per group of kGT blocks
   uint64_t *part = nullptr;    // scan partials, one per kPart blocks
@@ -1392,7 +1416,7 @@ int ensure_scratch(lz4r_ctx *c, size_t nb) {
   const size_t cap_slots = std::min(cap, kChunk);
   const size_t parts = (cap + kPart - 1) / kPart;
   const size_t groups = (cap + kGT - 1) / kGT;
-  // hipMalloc: 256-B aligned, so every slot is line-aligned
+  // hipMalloc: 256-B aligned; heads and overflow slots are 16-B multiples
   if (hipMalloc(&c->slots, cap_slots * (size_t)kSlot) != hipSuccess ||
       hipMalloc(&c->bsizes, cap * sizeof(uint16_t)) != hipSuccess ||
       hipMalloc(&c->boff, cap * sizeof(uint64_t)) != hipSuccess ||
@@ -1436,6 +1460,8 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   c->timed_chunks = nchunks;
   if (timed) (void)hipEventRecord(c->ev_a, s);
   const uint8_t *in = static_cast<const uint8_t *>(d_in);
+  // the block scratch: cap_slots heads of kHead bytes, then the overflow slots
+  uint8_t *const ovfs = c->slots + c->cap_slots * (size_t)kHead;
   for (size_t k = 0; k < nchunks; ++k) {
     const size_t b0 = k * kChunk;                      // first block of the chunk
     const size_t nbc = std::min(kChunk, nb - b0);
@@ -1449,12 +1475,12 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
     // (every chunk starts 300 b0 bytes in: a multiple of 4)
     if (((uintptr_t)in & 3) == 0) {
       hipLaunchKernelGGL(lz4_tiles<true>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
-                         (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0,
-                         c->status);
+                         (uint32_t)nbc, per, last_n, c->slots, ovfs, c->tsz + b0,
+                         c->bsizes + b0, c->status);
     } else
       hipLaunchKernelGGL(lz4_tiles<false>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
-                         (uint32_t)nbc, per, last_n, c->slots, c->tsz + b0, c->bsizes + b0,
-                         c->status);
+                         (uint32_t)nbc, per, last_n, c->slots, ovfs, c->tsz + b0,
+                         c->bsizes + b0, c->status);
     if (timed) (void)hipEventRecord(c->ev_tiles[2 * k + 1], s);
     const size_t p0 = b0 / kPart, np = (nbc + kPart - 1) / kPart;
     hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)np), dim3(256), 0, s, c->tsz, b1, p0,
@@ -1464,7 +1490,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
                        static_cast<uint64_t *>(d_len), c->verdict);
     const size_t g0 = b0 / kGT, ng = (nbc + kGT - 1) / kGT;
     hipLaunchKernelGGL(lz4_emit, dim3((unsigned)(ng * kGSplit)), dim3(64 * kEW), 0, s, in, c->slots,
-                       b0, c->tsz, b1, g0, c->gsum, c->part, static_cast<uint8_t *>(d_out),
+                       ovfs, b0, c->tsz, b1, g0, c->gsum, c->part, static_cast<uint8_t *>(d_out),
                        (uint64_t)cap, hdr, (uint64_t)nb, (uint32_t)(n - (nb - 1) * kBlk),
                        c->boff);
   }
