@@ -53,7 +53,7 @@ def compile_asm(src, extra=()):
 
 
 def kernel_range(L, name=KERNEL):
-    st = next(i for i, l in enumerate(L) if l.startswith(name) and l.split(":")[0].endswith("_"))
+    st = next(i for i, l in enumerate(L) if re.match(re.escape(name) + r"\S*:\s*(;.*)?$", l))
     en = next(i for i in range(st, len(L)) if L[i].startswith(".Lfunc_end"))
     return st, en
 
@@ -139,10 +139,16 @@ def instrument(L, st, en, kname):
     return txt, k
 
 
-def build(src=None, name="prod"):
+EMIT = "_ZN12_GLOBAL__N_18lz4_emit"
+
+
+def build(src=None, name="prod", kernel=KERNEL):
+    """kernel: KERNEL (lz4_tiles<true>) or EMIT (lz4_emit; name gets an "emit_" prefix)."""
     src = src or os.path.join(REPO, "lz4-jpeg_amd", "csrc", "lz4r.hip")
+    if kernel == EMIT:
+        name = "emit_" + name
     L = compile_asm(src)
-    st, en = kernel_range(L)
+    st, en = kernel_range(L, kernel)
     bbs = basic_blocks(L, st, en)
     kname = L[st].split(":")[0]
     txt, k = instrument(L, st, en, kname)
@@ -157,6 +163,83 @@ def build(src=None, name="prod"):
     json.dump({"kernel": kname, "bbs": bbs},
               open(os.path.join(OUT, f"bb_static_{name}.json"), "w"))
     print(f"{len(bbs)} basic blocks, {sum(len(b) for _, b in bbs)} static instructions")
+
+
+def _launch(hip, fn, grid, block, args):
+    params = (ctypes.c_void_p * len(args))(*[ctypes.cast(ctypes.pointer(a), ctypes.c_void_p)
+                                              for a in args])
+    assert hip.hipModuleLaunchKernel(fn, grid, 1, 1, block, 1, 1, 0, None, params, None) == 0
+
+
+def run_emit(outdir, name="prod", nbytes=1 << 30):
+    """The whole compressor from the module (lz4_tiles, the scans, the
+    instrumented lz4_emit) on the bench corpus; the stream must equal the
+    product library's."""
+    import hashlib
+    sys.path.insert(0, os.path.join(REPO, "lz4-jpeg_amd"))
+    import torch
+    from lz4jpeg import lz4, synth
+    hip = ctypes.CDLL("libamdhip64.so")
+    torch.cuda.init()
+    dev = torch.device("cuda", 0)
+    n = nbytes
+    d_in = torch.empty(n + 16, dtype=torch.uint8, device=dev)
+    synth.random_passages_device(d_in, n, length=30000, seed=1, first=0)
+    nb = (n + 299) // 300
+    last_n = n - (nb - 1) * 300
+    slots = torch.empty(nb * (96 + 400), dtype=torch.uint8, device=dev)
+    tsz = torch.empty(nb, dtype=torch.int32, device=dev)
+    bsz = torch.empty(nb, dtype=torch.int16, device=dev)
+    status = torch.zeros(4, dtype=torch.int64, device=dev)
+    npart = (nb + 4095) // 4096
+    gsum = torch.empty((nb + 63) // 64, dtype=torch.int32, device=dev)
+    part = torch.empty(npart, dtype=torch.int64, device=dev)
+    cap = 1 + nb * 548
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    boff = torch.empty(nb, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    mod = ctypes.c_void_p()
+    assert hip.hipModuleLoad(ctypes.byref(mod),
+                             os.path.join(OUT, f"bbcnt_emit_{name}.co").encode()) == 0
+    S = json.load(open(os.path.join(OUT, f"bb_static_emit_{name}.json")))
+    L = open(os.path.join(OUT, f"bbcnt_emit_{name}.s")).read()
+    fns = {}
+    for k in ("lz4_tilesILb1EE", "lz4_scan_reduce", "lz4_scan_partials", "lz4_emit"):
+        mangled = re.search(r"^(_ZN12_GLOBAL__N_1\d+" + k + r"\S*?):", L, re.M).group(1)
+        f = ctypes.c_void_p()
+        assert hip.hipModuleGetFunction(ctypes.byref(f), mod, mangled.encode()) == 0, k
+        fns[k] = f
+    acc, accsz = ctypes.c_void_p(), ctypes.c_size_t()
+    assert hip.hipModuleGetGlobal(ctypes.byref(acc), ctypes.byref(accsz), mod,
+                                  b"lz4r_bb_acc") == 0
+    assert hip.hipMemset(acc, 0, ctypes.c_size_t(4 * NCNT)) == 0
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    U32, U64, I32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+    per = (nb + 7) // 8
+    heads, ovfs = P(slots), ctypes.c_void_p(slots.data_ptr() + nb * 96)
+    _launch(hip, fns["lz4_tilesILb1EE"], 8 * per, 64,
+            [P(d_in), U32(nb), U32(per), U32(last_n), heads, ovfs, P(tsz), P(bsz), P(status)])
+    _launch(hip, fns["lz4_scan_reduce"], npart, 256, [P(tsz), U64(nb), U64(0), P(gsum), P(part)])
+    lenp = ctypes.c_void_p(status.data_ptr() + 8)
+    verd = ctypes.c_void_p(status.data_ptr() + 16)
+    _launch(hip, fns["lz4_scan_partials"], 1, 1024,
+            [P(part), U64(npart), U64(1), I32(1), I32(1), P(status), lenp, verd])
+    ng = (nb + 63) // 64
+    _launch(hip, fns["lz4_emit"], ng * 2, 512,
+            [P(d_in), heads, ovfs, U64(0), P(tsz), U64(nb), U64(0), P(gsum), P(part), P(out),
+             U64(cap), I32(1), U64(nb), U32(last_n), P(boff)])
+    assert hip.hipDeviceSynchronize() == 0
+    host = (ctypes.c_uint32 * NCNT)()
+    assert hip.hipMemcpy(host, acc, ctypes.c_size_t(4 * NCNT), 2) == 0
+    got = int(status[1].item())
+    comp = lz4.Compressor()
+    ref, rlen = comp.compress_device(d_in, n)
+    same = rlen == got and bool(torch.equal(ref[:rlen], out[:got]))
+    os.makedirs(outdir, exist_ok=True)
+    res = {"bytes": n, "blocks": nb, "workgroups": ng * 2, "stream_equal_product": same,
+           "counts": list(host)}
+    json.dump(res, open(os.path.join(outdir, f"bbcounts_emit_{name}.json"), "w"))
+    print(json.dumps({k: v for k, v in res.items() if k != "counts"}))
 
 
 def run(outdir, name="prod", nbytes=1 << 30):
@@ -307,6 +390,10 @@ if __name__ == "__main__":
     cmd = sys.argv[1]
     if cmd == "build":              # build [src.hip name]
         build(*sys.argv[2:4])
+    elif cmd == "build_emit":       # build_emit [src.hip name]
+        build(*(sys.argv[2:4] or [None, "prod"]), kernel=EMIT)
+    elif cmd == "run_emit":         # run_emit outdir [name]
+        run_emit(sys.argv[2], *sys.argv[3:4])
     elif cmd == "report":
         report(*sys.argv[2:5])
     elif cmd == "run":

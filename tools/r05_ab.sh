@@ -10,8 +10,12 @@ O=gpurun_out/r05ab
 mkdir -p $O
 [ -n "$AB_NORATE" ] || timeout -k 10 120 tools/ab/valu_rate > $O/valu_rate.log 2>&1 || exit 1
 for v in prod "$@"; do
-  [ -f tools/ab/bbcnt_$v.co ] || continue
-  timeout -k 10 120 python3 tools/bbcount.py run $O $v > $O/bbcount_$v.log 2>&1 || { tail -5 $O/bbcount_$v.log; exit 1; }
+  if [ -f tools/ab/bbcnt_$v.co ]; then
+    timeout -k 10 120 python3 tools/bbcount.py run $O $v > $O/bbcount_$v.log 2>&1 || { tail -5 $O/bbcount_$v.log; exit 1; }
+  fi
+  if [ -f tools/ab/bbcnt_emit_$v.co ]; then
+    timeout -k 10 120 python3 tools/bbcount.py run_emit $O $v > $O/bbcount_emit_$v.log 2>&1 || { tail -5 $O/bbcount_emit_$v.log; exit 1; }
+  fi
 done
 AB_NOPMC=1 bash tools/ab4.sh "$@"
 rc=$?
