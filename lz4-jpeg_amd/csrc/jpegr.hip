@@ -47,10 +47,10 @@ __constant__ double dAA88[8][8];
 __constant__ double dAA84[8][4];
 __constant__ int dLQ[64];
 __constant__ int dCQ[32];
-__constant__ double dLQr[64];   // RN(1 / T): the quantisation's fast path
-__constant__ double dCQr[32];
-__constant__ int dZZ8[64];
-__constant__ int dZZ4[32];
+__constant__ double dLK[64];    // RN(alpha_u alpha_v * RN(1 / T)): the quantisation's fast path
+__constant__ double dCK[32];
+__constant__ int dZZ8b[64];     // 2 * zigzag position: the int16's byte offset in the tile
+__constant__ int dZZ4b[32];
 __constant__ int dZZ8inv[64];   // zigzag index -> natural index
 __constant__ int dZZ4inv[32];
 
@@ -116,28 +116,31 @@ __device__ __forceinline__ void convert_pixel(uint32_t p, bool valid, int r,
 }
 
 // q = (int)(coef / T) (JPEG.c:626-627, IEEE division then truncation) for a
-// row of W coefficients.  r = RN(coef * RN(1/T)) and RN(coef / T) both lie
-// within ~1.5 ulp of coef / T (|r| < 2^12: ulp <= 2^-40), so their
-// truncations differ only when coef / T is that close to an integer; a lane
-// whose r is within 2^-30 of an integer (exact quotients and zeros included)
-// takes the IEEE division, the others truncate r.  The fallback is one
-// wave-uniform branch per row, so the division sequence runs only when some
-// lane of the wave needs it.
+// row of W coefficients coef = RN(aa * s) (JPEG.c:489).  The fast path is
+// r = RN(s * K) with K = RN(aa * RN(1/T)) (one multiply instead of two): r
+// lies within ~4 ulp of coef / T (|r| < 2^12: within 2^-39), so trunc(r) and
+// trunc(coef / T) differ only when coef / T is that close to an integer; a
+// lane whose r is within 2^-30 of an integer (exact quotients and zeros
+// included) takes the reference's path, coef = RN(aa * s) and the IEEE
+// division.  The near-integer tests collect into one SGPR lane mask (no
+// per-lane flag arithmetic), and the fallback runs behind one wave-uniform
+// branch, so the division sequence runs only when some lane of the wave
+// needs it.
 template <int W>
-__device__ __forceinline__ void quantize_row(const double (&cf)[W], const int *T,
-                                             const double *rT, int (&q)[W]) {
-  bool slow = false;
+__device__ __forceinline__ void quantize_row(const double (&sm)[W], const double *K,
+                                             const double *aa, const int *T, int (&q)[W]) {
+  uint64_t slow = 0;
 #pragma unroll
   for (int v = 0; v < W; ++v) {
-    const double r = cf[v] * rT[v];
-    slow = slow || !(fabs(r - __builtin_rint(r)) > 0x1p-30);
+    const double r = sm[v] * K[v];
+    slow |= __builtin_amdgcn_ballot_w64(!(fabs(r - __builtin_rint(r)) > 0x1p-30));
     q[v] = (int)r;
   }
-  if (__builtin_amdgcn_ballot_w64(slow)) {
+  if (slow) {
 #pragma unroll
     for (int v = 0; v < W; ++v) {
-      const int qd = (int)(cf[v] / (double)T[v]);
-      q[v] = slow ? qd : q[v];
+      const double r = sm[v] * K[v];
+      if (!(fabs(r - __builtin_rint(r)) > 0x1p-30)) q[v] = (int)((aa[v] * sm[v]) / (double)T[v]);
     }
   }
 }
@@ -222,13 +225,13 @@ __global__ __launch_bounds__(kEThreads) void jpeg_strip_kernel(
           s[v] = s[v] + tv * jpegr_tables::C8[y][v];             // *cos_y, +=
       }
     }
-    double cf[8];
+    if (RAW) {
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      cf[v] = dAA88[u][v] * s[v];                                // JPEG.c:489
-      if (RAW && tile_ok) static_cast<double *>(out)[tile_g * 128 + u * 8 + v] = cf[v];
+      for (int v = 0; v < 8; ++v)                                 // JPEG.c:489
+        if (tile_ok) static_cast<double *>(out)[tile_g * 128 + u * 8 + v] = dAA88[u][v] * s[v];
+    } else {
+      quantize_row<8>(s, &dLK[u * 8], &dAA88[u][0], &dLQ[u * 8], qy);   // JPEG.c:489, 626-627
     }
-    if (!RAW) quantize_row<8>(cf, &dLQ[u * 8], &dLQr[u * 8], qy);   // JPEG.c:626-627
 
   }
 
@@ -248,24 +251,29 @@ __global__ __launch_bounds__(kEThreads) void jpeg_strip_kernel(
         for (int v = 0; v < 4; ++v) s[v] = s[v] + tv * jpegr_tables::C4[y][v];
       }
     }
-    double cf[4];
+    if (RAW) {
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      cf[v] = dAA84[u][v] * s[v];
-      if (RAW && tile_ok) static_cast<double *>(out)[tile_g * 128 + 64 + ch * 32 + u * 4 + v] = cf[v];
+      for (int v = 0; v < 4; ++v)
+        if (tile_ok)
+          static_cast<double *>(out)[tile_g * 128 + 64 + ch * 32 + u * 4 + v] = dAA84[u][v] * s[v];
+    } else {
+      quantize_row<4>(s, &dCK[u * 4], &dAA84[u][0], &dCQ[u * 4], qc[ch]);
     }
-    if (!RAW) quantize_row<4>(cf, &dCQ[u * 4], &dCQr[u * 4], qc[ch]);
   }
 
   if (RAW) return;
   __syncthreads();                   // every thread is done reading the samples
+  {
+    // zigzag (JPEG.c:693-728) by byte offsets from the tables
+    uint8_t *const ob = reinterpret_cast<uint8_t *>(olds) + tile * 256;
 #pragma unroll
-  for (int v = 0; v < 8; ++v) olds[tile * 128 + dZZ8[u * 8 + v]] = (int16_t)qy[v];
+    for (int v = 0; v < 8; ++v) *reinterpret_cast<int16_t *>(ob + dZZ8b[u * 8 + v]) = (int16_t)qy[v];
 #pragma unroll
-  for (int ch = 0; ch < 2; ++ch)
+    for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
-    for (int v = 0; v < 4; ++v)
-      olds[tile * 128 + 64 + ch * 32 + dZZ4[u * 4 + v]] = (int16_t)qc[ch][v];
+      for (int v = 0; v < 4; ++v)
+        *reinterpret_cast<int16_t *>(ob + 128 + ch * 64 + dZZ4b[u * 4 + v]) = (int16_t)qc[ch][v];
+  }
   __syncthreads();
 
   // ---- phase 4: coalesced store of the strip's tiles -------------------------
@@ -477,13 +485,17 @@ hipError_t upload_tables() {
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dAA84), AA84, sizeof(AA84))) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dLQ), lq, sizeof(lq))) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dCQ), cq, sizeof(cq))) != hipSuccess) return e;
-  double lqr[64], cqr[32];
-  for (int i = 0; i < 64; ++i) lqr[i] = 1.0 / (double)lq[i];    // correctly rounded
-  for (int i = 0; i < 32; ++i) cqr[i] = 1.0 / (double)cq[i];
-  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dLQr), lqr, sizeof(lqr))) != hipSuccess) return e;
-  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dCQr), cqr, sizeof(cqr))) != hipSuccess) return e;
-  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ8), z8, sizeof(z8))) != hipSuccess) return e;
-  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ4), z4, sizeof(z4))) != hipSuccess) return e;
+  // K = RN(alpha_u alpha_v * RN(1 / T)), both IEEE double operations
+  double lk[64], ck[32];
+  for (int i = 0; i < 64; ++i) lk[i] = AA88[i / 8][i % 8] * (1.0 / (double)lq[i]);
+  for (int i = 0; i < 32; ++i) ck[i] = AA84[i / 4][i % 4] * (1.0 / (double)cq[i]);
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dLK), lk, sizeof(lk))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dCK), ck, sizeof(ck))) != hipSuccess) return e;
+  int z8b[64], z4b[32];
+  for (int i = 0; i < 64; ++i) z8b[i] = 2 * z8[i];
+  for (int i = 0; i < 32; ++i) z4b[i] = 2 * z4[i];
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ8b), z8b, sizeof(z8b))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ4b), z4b, sizeof(z4b))) != hipSuccess) return e;
   int i8[64], i4[32];
   for (int i = 0; i < 64; ++i) i8[ZZ8_POS[i]] = i;
   for (int i = 0; i < 32; ++i) i4[ZZ4_POS[i]] = i;
