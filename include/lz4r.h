@@ -201,9 +201,15 @@ int lz4r_check(lz4r_ctx *ctx, void *stream);
  * own launch stream around the whole call and around each launch of the
  * compressor kernel lz4_tiles (one per 2^24-block chunk of the input).
  * lz4r_last_timing waits for the last call's end event and returns the
- * call's duration and the summed lz4_tiles durations in milliseconds. */
+ * call's duration and the summed lz4_tiles durations in milliseconds.
+ * Enabling starts a new record; each timed call has its own events (a ring
+ * of the newest 4096 calls), so back-to-back async calls are timed without a
+ * host wait between them: lz4r_timed_calls then waits for the newest call and
+ * fills ms_call/ms_match with the newest min(calls, 4096, max) calls' times,
+ * oldest first, and their number in *count. */
 int lz4r_set_timing(lz4r_ctx *ctx, int enable);
 int lz4r_last_timing(lz4r_ctx *ctx, float *ms_call, float *ms_match);
+int lz4r_timed_calls(lz4r_ctx *ctx, size_t max, float *ms_call, float *ms_match, size_t *count);
 
 const char *lz4r_strerror(int code);
 

@@ -1381,13 +1381,19 @@ struct lz4r_ctx {
   uint64_t *verdict = nullptr; // (len + 2) the last call's corrupt-index verdict (0 / 1)
   size_t last_nb = 0;
   bool checkable = false;      // a call has launched (lz4r_check has a verdict to read)
-  // timing: the call's start/end, and lz4_tiles' start/end in every chunk
-  hipEvent_t ev_a = nullptr, ev_c = nullptr;
-  std::vector<hipEvent_t> ev_tiles;   // 2 per chunk
-  size_t timed_chunks = 0;
+  // timing: per timed call since lz4r_set_timing(1), the call's start/end
+  // events and lz4_tiles' start/end in every chunk (a ring of kTimedCalls
+  // sets, so back-to-back async calls need no host wait between them)
+  struct timed_set {
+    hipEvent_t a = nullptr, c = nullptr;
+    std::vector<hipEvent_t> tiles;   // 2 per chunk
+    size_t chunks = 0;
+  };
+  std::vector<timed_set> tsets;
+  size_t timed_calls = 0;      // calls recorded since timing was enabled
   bool timing = false;
-  bool timed_call = false;     // the last call recorded the events
 };
+constexpr size_t kTimedCalls = 4096;
 
 namespace {
 
@@ -1432,12 +1438,45 @@ int ensure_scratch(lz4r_ctx *c, size_t nb) {
   return LZ4R_OK;
 }
 
-int ensure_events(lz4r_ctx *c, size_t nchunks) {
-  while (c->ev_tiles.size() < 2 * nchunks) {
+// the event set of the next timed call (created on first use)
+int next_timed_set(lz4r_ctx *c, size_t nchunks, lz4r_ctx::timed_set **out) {
+  const size_t i = c->timed_calls % kTimedCalls;
+  if (c->tsets.size() <= i) c->tsets.resize(i + 1);
+  lz4r_ctx::timed_set &t = c->tsets[i];
+  if ((!t.a && hipEventCreate(&t.a) != hipSuccess) || (!t.c && hipEventCreate(&t.c) != hipSuccess))
+    return LZ4R_ERR_HIP;
+  while (t.tiles.size() < 2 * nchunks) {
     hipEvent_t e = nullptr;
     if (hipEventCreate(&e) != hipSuccess) return LZ4R_ERR_HIP;
-    c->ev_tiles.push_back(e);
+    t.tiles.push_back(e);
   }
+  t.chunks = nchunks;
+  *out = &t;
+  return LZ4R_OK;
+}
+
+void destroy_events(lz4r_ctx *c) {
+  for (auto &t : c->tsets) {
+    if (t.a) (void)hipEventDestroy(t.a);
+    if (t.c) (void)hipEventDestroy(t.c);
+    for (hipEvent_t e : t.tiles) (void)hipEventDestroy(e);
+  }
+  c->tsets.clear();
+}
+
+// milliseconds of timed call set t: the whole call and its lz4_tiles launches
+int timed_ms(const lz4r_ctx::timed_set &t, float *ms_call, float *ms_match) {
+  if (hipEventSynchronize(t.c) != hipSuccess) return LZ4R_ERR_HIP;
+  float a = 0.f, b = 0.f;
+  if (hipEventElapsedTime(&a, t.a, t.c) != hipSuccess) return LZ4R_ERR_HIP;
+  for (size_t k = 0; k < t.chunks; ++k) {
+    float x = 0.f;
+    if (hipEventElapsedTime(&x, t.tiles[2 * k], t.tiles[2 * k + 1]) != hipSuccess)
+      return LZ4R_ERR_HIP;
+    b += x;
+  }
+  *ms_call = a;
+  *ms_match = b;
   return LZ4R_OK;
 }
 
@@ -1455,10 +1494,9 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   static_assert(kPart % kGT == 0, "partials hold whole groups");
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool timed = c->timing;
-  if (timed && (rc = ensure_events(c, nchunks)) != LZ4R_OK) return rc;
-  c->timed_call = timed;
-  c->timed_chunks = nchunks;
-  if (timed) (void)hipEventRecord(c->ev_a, s);
+  lz4r_ctx::timed_set *ts = nullptr;
+  if (timed && (rc = next_timed_set(c, nchunks, &ts)) != LZ4R_OK) return rc;
+  if (timed) (void)hipEventRecord(ts->a, s);
   const uint8_t *in = static_cast<const uint8_t *>(d_in);
   // the block scratch: cap_slots heads of kHead bytes, then the overflow slots
   uint8_t *const ovfs = c->slots + c->cap_slots * (size_t)kHead;
@@ -1471,7 +1509,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
     // per-block cost (a static grid-stride split leaves a tail; measured
     // slower also with the next block prefetched into registers)
     const uint32_t per = (uint32_t)((nbc + 7) / 8);    // blocks per XCD slice
-    if (timed) (void)hipEventRecord(c->ev_tiles[2 * k], s);
+    if (timed) (void)hipEventRecord(ts->tiles[2 * k], s);
     // (every chunk starts 300 b0 bytes in: a multiple of 4)
     if (((uintptr_t)in & 3) == 0) {
       hipLaunchKernelGGL(lz4_tiles<true>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
@@ -1481,7 +1519,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
       hipLaunchKernelGGL(lz4_tiles<false>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
                          (uint32_t)nbc, per, last_n, c->slots, ovfs, c->tsz + b0,
                          c->bsizes + b0, c->status);
-    if (timed) (void)hipEventRecord(c->ev_tiles[2 * k + 1], s);
+    if (timed) (void)hipEventRecord(ts->tiles[2 * k + 1], s);
     const size_t p0 = b0 / kPart, np = (nbc + kPart - 1) / kPart;
     hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)np), dim3(256), 0, s, c->tsz, b1, p0,
                        c->gsum, c->part);
@@ -1494,7 +1532,10 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
                        (uint64_t)cap, hdr, (uint64_t)nb, (uint32_t)(n - (nb - 1) * kBlk),
                        c->boff);
   }
-  if (timed) (void)hipEventRecord(c->ev_c, s);
+  if (timed) {
+    (void)hipEventRecord(ts->c, s);
+    ++c->timed_calls;
+  }
   c->last_nb = nb;
   c->checkable = true;
   const hipError_t e = hipGetLastError();
@@ -1527,8 +1568,7 @@ int lz4r_ctx_create(lz4r_ctx **out) {
   if (!c) return LZ4R_ERR_NOMEM;
   if (hipGetDevice(&c->device) != hipSuccess ||
       hipMalloc(&c->len, 3 * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(c->len, 0, 3 * sizeof(uint64_t)) != hipSuccess ||
-      hipEventCreate(&c->ev_a) != hipSuccess || hipEventCreate(&c->ev_c) != hipSuccess) {
+      hipMemset(c->len, 0, 3 * sizeof(uint64_t)) != hipSuccess) {
     lz4r_ctx_destroy(c);
     return LZ4R_ERR_HIP;
   }
@@ -1542,9 +1582,7 @@ void lz4r_ctx_destroy(lz4r_ctx *c) {
   if (!c) return;
   free_scratch(c);
   (void)hipFree(c->len);
-  if (c->ev_a) (void)hipEventDestroy(c->ev_a);
-  if (c->ev_c) (void)hipEventDestroy(c->ev_c);
-  for (hipEvent_t e : c->ev_tiles) (void)hipEventDestroy(e);
+  destroy_events(c);
   delete c;
 }
 
@@ -1566,11 +1604,16 @@ int lz4r_compress_segment_async(lz4r_ctx *c, const void *d_in, size_t n, void *d
   if (n == 0) {                      // an empty shard (more ranks than blocks)
     c->last_nb = 0;
     c->checkable = false;     // nothing launched: lz4r_check reports OK
-    c->timed_call = false;
-    return hipMemsetAsync(d_len, 0, sizeof(uint64_t), static_cast<hipStream_t>(stream)) ==
-                   hipSuccess
-               ? LZ4R_OK
-               : LZ4R_ERR_HIP;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (c->timing) {          // a timed call of no launches
+      lz4r_ctx::timed_set *ts = nullptr;
+      const int rc = next_timed_set(c, 0, &ts);
+      if (rc != LZ4R_OK) return rc;
+      (void)hipEventRecord(ts->a, s);
+      (void)hipEventRecord(ts->c, s);
+      ++c->timed_calls;
+    }
+    return hipMemsetAsync(d_len, 0, sizeof(uint64_t), s) == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
   }
   return run(c, d_in, n, d_out, cap, d_len, 0, stream);
 }
@@ -1692,22 +1735,30 @@ int lz4r_check(lz4r_ctx *c, void *stream) {
 int lz4r_set_timing(lz4r_ctx *c, int enable) {
   if (!c) return LZ4R_ERR_ARG;
   c->timing = enable != 0;
+  if (c->timing) c->timed_calls = 0;
   return LZ4R_OK;
 }
 
 int lz4r_last_timing(lz4r_ctx *c, float *ms_call, float *ms_match) {
-  if (!c || !c->timed_call) return LZ4R_ERR_ARG;
-  if (hipEventSynchronize(c->ev_c) != hipSuccess) return LZ4R_ERR_HIP;
+  if (!c || c->timed_calls == 0) return LZ4R_ERR_ARG;
   float a = 0.f, b = 0.f;
-  if (hipEventElapsedTime(&a, c->ev_a, c->ev_c) != hipSuccess) return LZ4R_ERR_HIP;
-  for (size_t k = 0; k < c->timed_chunks; ++k) {
-    float t = 0.f;
-    if (hipEventElapsedTime(&t, c->ev_tiles[2 * k], c->ev_tiles[2 * k + 1]) != hipSuccess)
-      return LZ4R_ERR_HIP;
-    b += t;
-  }
+  const int rc = timed_ms(c->tsets[(c->timed_calls - 1) % kTimedCalls], &a, &b);
+  if (rc != LZ4R_OK) return rc;
   if (ms_call) *ms_call = a;
   if (ms_match) *ms_match = b;
+  return LZ4R_OK;
+}
+
+int lz4r_timed_calls(lz4r_ctx *c, size_t max, float *ms_call, float *ms_match, size_t *count) {
+  if (!c || !count || (max && (!ms_call || !ms_match))) return LZ4R_ERR_ARG;
+  // the newest min(calls, ring, max) calls, oldest first
+  const size_t n = std::min(std::min(c->timed_calls, kTimedCalls), max);
+  for (size_t j = 0; j < n; ++j) {
+    const size_t i = (c->timed_calls - n + j) % kTimedCalls;
+    const int rc = timed_ms(c->tsets[i], &ms_call[j], &ms_match[j]);
+    if (rc != LZ4R_OK) return rc;
+  }
+  *count = n;
   return LZ4R_OK;
 }
 

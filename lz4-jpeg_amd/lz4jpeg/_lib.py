@@ -38,6 +38,8 @@ SIGNATURES = [
     ("lz4r_check", _i, [_vp, _vp]),
     ("lz4r_set_timing", _i, [_vp, _i]),
     ("lz4r_last_timing", _i, [_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+    ("lz4r_timed_calls", _i, [_vp, _c_size, ctypes.POINTER(ctypes.c_float),
+                              ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_c_size)]),
     ("lz4r_strerror", ctypes.c_char_p, [_i]),
     # jpegr.h
     ("jpegr_coef_count", _c_size, [_i, _i]),

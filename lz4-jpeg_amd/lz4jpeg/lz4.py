@@ -158,6 +158,18 @@ class Compressor:
             _raise(rc, "lz4r_last_timing")
         return a.value, b.value
 
+    def timed_calls(self, max_calls=4096):
+        """(ms of each call, ms of its lz4_tiles launches): two lists over the
+        newest calls timed since set_timing(True), oldest first (waits for
+        the newest; lz4r_timed_calls)."""
+        a = (ctypes.c_float * max_calls)()
+        b = (ctypes.c_float * max_calls)()
+        cnt = ctypes.c_size_t(0)
+        rc = _lib.lib().lz4r_timed_calls(self._h, max_calls, a, b, ctypes.byref(cnt))
+        if rc != 0:
+            _raise(rc, "lz4r_timed_calls")
+        return list(a[:cnt.value]), list(b[:cnt.value])
+
     # -- host convenience -------------------------------------------------
     def compress(self, data):
         """bytes -> framed compressed bytes (== the reference's compressed.bin)."""

@@ -148,6 +148,35 @@ def test_check_reads_the_contexts_own_verdict(comp):
     assert comp.async_length(d_len) == 0
 
 
+def test_timed_back_to_back_async_calls(comp, oracle):
+    """Timing of stream-ordered async calls (the bench's N = 1 step): every
+    call has its own events, read after the last one; an empty segment is a
+    timed call of no launches; the last call's output equals the oracle's."""
+    import torch
+    from lz4jpeg.lz4 import compress_bound
+    data = golden_inputs.lz4_input("metamorphosis_spaces") * 40
+    d_in = torch.from_numpy(np.frombuffer(bytes(data), dtype=np.uint8).copy()).cuda()
+    d_out = torch.empty(compress_bound(len(data)), dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(1, dtype=torch.int64, device="cuda")
+    comp.set_timing(True)
+    try:
+        for _ in range(7):
+            comp.compress_async(d_in, len(data), d_out, d_len)
+        calls, tiles = comp.timed_calls()
+        assert len(calls) == 7 and all(0 < t <= c for c, t in zip(calls, tiles))
+        assert comp.timed_calls(3)[0] == calls[-3:]
+        comp.compress_async(d_in, 0, d_out, d_len, segment=True, final_shard=True)
+        calls, tiles = comp.timed_calls()
+        assert len(calls) == 8 and tiles[-1] == 0.0
+        comp.set_timing(True)                       # a new record
+        comp.compress_async(d_in, len(data), d_out, d_len)
+        assert len(comp.timed_calls()[0]) == 1
+        n = comp.async_length(d_len)
+    finally:
+        comp.set_timing(False)
+    assert d_out[:n].cpu().numpy().tobytes() == oracle.lz4_compress(bytes(data))
+
+
 def test_segments_concatenate_to_stream(comp, oracle):
     """Shard outputs (lz4r_compress_segment_async) + header byte == framed stream."""
     import torch
