@@ -418,6 +418,22 @@ __device__ __forceinline__ void store_lanes1(uint64_t m, uint32_t *base, uint32_
       : "memory", "scc");
 }
 
+// S.buf[kOff + addr] = v (a dword) in the lanes of m, the same way: no
+// select of a dummy address for the other lanes (the wave's LDS operations
+// are served in order, so later reads see the store; lz4_tiles' TileLds sits
+// at LDS address 0, as xchg_rtn5's offsets assume)
+template <int kOff>
+__device__ __forceinline__ void lds_store_lanes(uint64_t m, uint32_t addr, uint32_t v) {
+  uint64_t save;
+  asm volatile(
+      "s_and_saveexec_b64 %0, %1\n\t"
+      "ds_write_b32 %2, %3 offset:%c4\n\t"
+      "s_or_b64 exec, exec, %0"
+      : "=&s"(save)
+      : "s"(m), "v"(addr), "v"(v), "i"(kOff)
+      : "memory", "scc");
+}
+
 // The compressor's workgroup is one wave.  A wave's LDS operations are
 // served in order, so its phase boundaries need neither s_barrier nor the
 // s_waitcnt vmcnt(0) lgkmcnt(0) that __syncthreads() implies: a compiler
@@ -486,15 +502,21 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
       // one global_load_dwordx2 (kFull) or ds_read2_b32
       const uint32_t w1 = bw[16 * r], w2 = bw[16 * r + 1];
       key[r] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-      // blk[p - 1] = byte 0 of key(p - 1): the lane below's key (DPP
-      // wave_shr:1), for lane 0 lane 63's key of the round before (round 0's
-      // lane 0 is p = 0, whose byte is the sentinel bit below)
-      const uint32_t below = r ? (uint32_t)__builtin_amdgcn_readlane((int)key[r - 1], 63) : 0u;
-      const uint32_t pb = (uint32_t)__builtin_amdgcn_update_dpp((int)below, (int)key[r], 0x138,
-                                                               0xf, 0xf, false);
       const uint32_t hv = key[r] * 2654435761u;                    // bucket = top 10 bits
-      // [0, 0, blk[p - 1], hash bits 16..23]: the entry without its link
-      pt[r] = __builtin_amdgcn_perm(pb, hv, 0x02040C0Cu);
+      if (r == 0) {
+        // blk[p - 1] = byte 0 of the lane below's key (DPP wave_shr:1; lane 0
+        // is p = 0, whose byte is the sentinel bit below)
+        const uint32_t pb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key[0], 0x138, 0xf,
+                                                                 0xf, false);
+        // [0, 0, blk[p - 1], hash bits 16..23]: the entry without its link
+        pt[0] = __builtin_amdgcn_perm(pb, hv, 0x02040C0Cu);
+      } else {
+        // rows 1..4: blk[p - 1] is byte 3 + sh of the dword pair before
+        // (one more dword in the same load, no cross-lane step)
+        const uint32_t w0 = bw[16 * r - 1];
+        const uint32_t pb = __builtin_amdgcn_perm(w1, w0, 0x0C0C0C03u + sh);
+        pt[r] = __builtin_amdgcn_perm(pb, hv, 0x02040C0Cu);
+      }
       const int p = 64 * r + lane;
       // (full block: rounds 0..3 are all 4-gram starts)
       const bool act = search && ((kFull && r < 4) || p < nk);
@@ -533,11 +555,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
 #pragma unroll
     for (int r = 4; r >= 0; --r) {
       const uint64_t m = ballot(walk[r]);
-      // branch-free: a lane without a walker writes its own dword of the idle
-      // candidate list (the select reads the mask straight from SGPRs)
-      const uint32_t at = sel_mask(m, (rank_below_plus(m, qn) << 2) + kQOff,
-                                   (uint32_t)(kCandOff + 4 * lane));
-      *reinterpret_cast<uint32_t *>(S.buf + at) = set[r];
+      // only the walkers' lanes store (EXEC = m around the store)
+      lds_store_lanes<kQOff>(m, rank_below_plus(m, qn) << 2, set[r]);
       qn += (uint32_t)__popcll(m);
     }
     ent_store_rec_zero_addtid(e);        // ent[64 r + lane] = e[r]; rec[] = 0
@@ -597,7 +616,6 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
     int qrd4 = 0;
     const int qwr4 = 4 * qwr;
     const uint8_t *const qb = reinterpret_cast<const uint8_t *>(S.q());
-    uint8_t *const cb = reinterpret_cast<uint8_t *>(S.cand());
     int a = 0, b = 0;
     uint32_t me = 0;                       // the walker's own entry (re-read only on a take)
     uint64_t vm = 0;                       // lanes holding a walker
@@ -605,10 +623,9 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
     auto pass = [&]() {
       const uint32_t o = ent_at(b);
       const uint64_t cm = vm & ballot(((me ^ o) - (1u << 15)) < (1u << 24) - (1u << 15));
-      const int sl4 =
-          (int)sel_mask(cm, (uint32_t)(4 * ncand + (rank_below(cm) << 2)), (uint32_t)(4 * kTrash));
       // the pair (walker, chain entry): the entry is the earlier position
-      *reinterpret_cast<uint32_t *>(cb + sl4) = (uint32_t)a | ((uint32_t)b << 16);
+      lds_store_lanes<kCandOff>(cm, rank_below_plus(cm, (uint32_t)ncand) << 2,
+                                (uint32_t)a | ((uint32_t)b << 16));
       ncand += __popcll(cm);
       const int bn = (int)(o & 2047u);
       vm &= ballot(bn < b);                // the chain ends (kNoLink, or any non-decreasing link)

@@ -8,8 +8,8 @@ export TMPDIR=/tmp
 O=gpurun_out/r05round
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 && \
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $O/bench.json 2> $O/bench.err && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.log && \
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.log && \
 python3 tools/prof_summary.py $O/prof > $O/kernels.md && \
 bash tools/traffic.sh > $O/traffic.log 2>&1 && \
 bash tools/r05_roof.sh > $O/roof.log 2>&1 && \
