@@ -1403,7 +1403,7 @@ struct lz4r_ctx {
   // sets, so back-to-back async calls need no host wait between them)
   struct timed_set {
     hipEvent_t a = nullptr, c = nullptr;
-    std::vector<hipEvent_t> tiles;   // 2 per chunk
+    std::vector<hipEvent_t> tiles;   // 2 per chunk (chunk 0 starts at a: tiles[0] unused)
     size_t chunks = 0;
   };
   std::vector<timed_set> tsets;
@@ -1455,16 +1455,25 @@ int ensure_scratch(lz4r_ctx *c, size_t nb) {
   return LZ4R_OK;
 }
 
+// A timing event: no system-scope fence when it is recorded (the events only
+// time the work; the call's results reach the host by their own copies).  With
+// the default fence every record writes back and invalidates the caches: four
+// records cost a back-to-back call 13 us (tools/timing_cost.py).
+int make_event(hipEvent_t *e) {
+  return hipEventCreateWithFlags(e, hipEventDisableSystemFence) == hipSuccess ? LZ4R_OK
+                                                                               : LZ4R_ERR_HIP;
+}
+
 // the event set of the next timed call (created on first use)
 int next_timed_set(lz4r_ctx *c, size_t nchunks, lz4r_ctx::timed_set **out) {
   const size_t i = c->timed_calls % kTimedCalls;
   if (c->tsets.size() <= i) c->tsets.resize(i + 1);
   lz4r_ctx::timed_set &t = c->tsets[i];
-  if ((!t.a && hipEventCreate(&t.a) != hipSuccess) || (!t.c && hipEventCreate(&t.c) != hipSuccess))
+  if ((!t.a && make_event(&t.a) != LZ4R_OK) || (!t.c && make_event(&t.c) != LZ4R_OK))
     return LZ4R_ERR_HIP;
   while (t.tiles.size() < 2 * nchunks) {
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return LZ4R_ERR_HIP;
+    if (make_event(&e) != LZ4R_OK) return LZ4R_ERR_HIP;
     t.tiles.push_back(e);
   }
   t.chunks = nchunks;
@@ -1488,7 +1497,7 @@ int timed_ms(const lz4r_ctx::timed_set &t, float *ms_call, float *ms_match) {
   if (hipEventElapsedTime(&a, t.a, t.c) != hipSuccess) return LZ4R_ERR_HIP;
   for (size_t k = 0; k < t.chunks; ++k) {
     float x = 0.f;
-    if (hipEventElapsedTime(&x, t.tiles[2 * k], t.tiles[2 * k + 1]) != hipSuccess)
+    if (hipEventElapsedTime(&x, k == 0 ? t.a : t.tiles[2 * k], t.tiles[2 * k + 1]) != hipSuccess)
       return LZ4R_ERR_HIP;
     b += x;
   }
@@ -1526,7 +1535,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
     // per-block cost (a static grid-stride split leaves a tail; measured
     // slower also with the next block prefetched into registers)
     const uint32_t per = (uint32_t)((nbc + 7) / 8);    // blocks per XCD slice
-    if (timed) (void)hipEventRecord(ts->tiles[2 * k], s);
+    if (timed && k > 0) (void)hipEventRecord(ts->tiles[2 * k], s);   // chunk 0 starts at ts->a
     // (every chunk starts 300 b0 bytes in: a multiple of 4)
     if (((uintptr_t)in & 3) == 0) {
       hipLaunchKernelGGL(lz4_tiles<true>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
