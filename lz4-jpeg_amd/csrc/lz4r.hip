@@ -70,6 +70,7 @@
 // HBM traffic per input byte: 1 B read + ~0.35 B of records written by
 // lz4_tiles; ~1 B of input + ~0.33 B of record heads read and ~1.03 B
 // written by lz4_emit (+14 B/block of sizes and offsets).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <limits.h>
 #include <stdint.h>
@@ -1522,7 +1523,11 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
   const bool timed = c->timing;
   lz4r_ctx::timed_set *ts = nullptr;
   if (timed && (rc = next_timed_set(c, nchunks, &ts)) != LZ4R_OK) return rc;
-  if (timed) (void)hipEventRecord(ts->a, s);
+  // A timed call's events ride on its kernels' own dispatch packets
+  // (hipExtLaunchKernelGGL: start / stop timestamps of the dispatch), so
+  // timing adds no marker packet between the kernels: call = the first
+  // lz4_tiles start .. the last lz4_emit stop.
+  auto ev = [&](hipEvent_t e) { return timed ? e : nullptr; };
   const uint8_t *in = static_cast<const uint8_t *>(d_in);
   // the block scratch: cap_slots heads of kHead bytes, then the overflow slots
   uint8_t *const ovfs = c->slots + c->cap_slots * (size_t)kHead;
@@ -1535,17 +1540,17 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
     // per-block cost (a static grid-stride split leaves a tail; measured
     // slower also with the next block prefetched into registers)
     const uint32_t per = (uint32_t)((nbc + 7) / 8);    // blocks per XCD slice
-    if (timed && k > 0) (void)hipEventRecord(ts->tiles[2 * k], s);   // chunk 0 starts at ts->a
+    hipEvent_t t0 = timed ? (k == 0 ? ts->a : ts->tiles[2 * k]) : nullptr;   // chunk 0 starts the call
+    hipEvent_t t1 = timed ? ts->tiles[2 * k + 1] : nullptr;
     // (every chunk starts 300 b0 bytes in: a multiple of 4)
     if (((uintptr_t)in & 3) == 0) {
-      hipLaunchKernelGGL(lz4_tiles<true>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
-                         (uint32_t)nbc, per, last_n, c->slots, ovfs, c->tsz + b0,
-                         c->bsizes + b0, c->status);
+      hipExtLaunchKernelGGL(lz4_tiles<true>, dim3(8 * per), dim3(64), 0, s, t0, t1, 0u,
+                            in + b0 * kBlk, (uint32_t)nbc, per, last_n, c->slots, ovfs,
+                            c->tsz + b0, c->bsizes + b0, c->status);
     } else
-      hipLaunchKernelGGL(lz4_tiles<false>, dim3(8 * per), dim3(64), 0, s, in + b0 * kBlk,
-                         (uint32_t)nbc, per, last_n, c->slots, ovfs, c->tsz + b0,
-                         c->bsizes + b0, c->status);
-    if (timed) (void)hipEventRecord(ts->tiles[2 * k + 1], s);
+      hipExtLaunchKernelGGL(lz4_tiles<false>, dim3(8 * per), dim3(64), 0, s, t0, t1, 0u,
+                            in + b0 * kBlk, (uint32_t)nbc, per, last_n, c->slots, ovfs,
+                            c->tsz + b0, c->bsizes + b0, c->status);
     const size_t p0 = b0 / kPart, np = (nbc + kPart - 1) / kPart;
     hipLaunchKernelGGL(lz4_scan_reduce, dim3((unsigned)np), dim3(256), 0, s, c->tsz, b1, p0,
                        c->gsum, c->part);
@@ -1553,15 +1558,14 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
                        (uint64_t)hdr, k == 0 ? 1 : 0, k + 1 == nchunks ? 1 : 0, c->status,
                        static_cast<uint64_t *>(d_len), c->verdict);
     const size_t g0 = b0 / kGT, ng = (nbc + kGT - 1) / kGT;
-    hipLaunchKernelGGL(lz4_emit, dim3((unsigned)(ng * kGSplit)), dim3(64 * kEW), 0, s, in, c->slots,
-                       ovfs, b0, c->tsz, b1, g0, c->gsum, c->part, static_cast<uint8_t *>(d_out),
-                       (uint64_t)cap, hdr, (uint64_t)nb, (uint32_t)(n - (nb - 1) * kBlk),
-                       c->boff);
+    hipExtLaunchKernelGGL(lz4_emit, dim3((unsigned)(ng * kGSplit)), dim3(64 * kEW), 0, s, nullptr,
+                          k + 1 == nchunks ? ev(ts ? ts->c : nullptr) : nullptr, 0u, in,
+                          (const uint8_t *)c->slots, (const uint8_t *)ovfs, b0,
+                          (const uint32_t *)c->tsz, b1, g0, (const uint32_t *)c->gsum,
+                          (const uint64_t *)c->part, static_cast<uint8_t *>(d_out), (uint64_t)cap,
+                          hdr, (uint64_t)nb, (uint32_t)(n - (nb - 1) * kBlk), c->boff);
   }
-  if (timed) {
-    (void)hipEventRecord(ts->c, s);
-    ++c->timed_calls;
-  }
+  if (timed) ++c->timed_calls;
   c->last_nb = nb;
   c->checkable = true;
   const hipError_t e = hipGetLastError();
