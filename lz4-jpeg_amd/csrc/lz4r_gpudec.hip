@@ -432,7 +432,11 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
     const int nv = (int)(total >> 4);
     const uint4 *src = reinterpret_cast<const uint4 *>(S.out);
     uint4 *dst = reinterpret_cast<uint4 *>(out + o0);
-    for (int v = lane; v < nv; v += kLanes) dst[v] = src[v];
+    // written once: non-temporal 16-B stores (-1.3 %, tools/ab_dec_inproc.py)
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    for (int v = lane; v < nv; v += kLanes)
+      __builtin_nontemporal_store(reinterpret_cast<const u32x4 *>(src)[v],
+                                  reinterpret_cast<u32x4 *>(dst) + v);
     for (size_t i = (size_t)nv * 16 + lane; i < total; i += kLanes) out[o0 + i] = S.out[i];
   } else {
     for (size_t i = lane; i < total; i += kLanes) out[o0 + i] = S.out[i];
