@@ -18,7 +18,7 @@
 //            into it (ds_wrxchg_rtn_b32) in ascending position order and keeps
 //            the old head as its link (byte offsets 4 p), so every chain
 //            strictly decreases; entry = link | (p == 0) << 15 | preceding
-//            byte << 16 | tag << 24, stored by add-TID (address = lane).
+//            byte << 16 | own byte (the tag) << 24, stored by add-TID.
 //     local  every unordered pair of a bucket is met once, by the later
 //            position walking its chain (deepest walkers first); a lane
 //            keeps its walker until the chain ends -- or a link fails to
@@ -57,7 +57,7 @@
 // round = 64 sequences of one or more blocks), and the bytes of write_block /
 // write_sequence (LZ4.c:365-425) land by aligned ds_or in a zeroed LDS image
 // of the output range -- header bytes from the sequence lanes, literal runs
-// flattened over the lanes as aligned 8-byte words -- which leaves as aligned
+// flattened over the lanes as aligned 16-byte words -- which leaves as aligned
 // 16-B stores.  Splitting the emission off lz4_tiles (which is bound by
 // instruction issue, one block per wave) lets a round of lz4_emit serve
 // several blocks: lz4_tiles 3.44 -> 2.97 ms per GiB, and the slot round trip
@@ -168,7 +168,7 @@ static_assert(kHead % 16 == 0 && kOvf % 16 == 0 && 4 * (121 + 1 - kHeadW) <= kOv
 struct TileLds {
   alignas(16) uint8_t buf[kBufBytes];
   union {
-    uint32_t ent[kArr];   // per position: link | tag << 17 | preceding byte << 22
+    uint32_t ent[kArr];   // per position: link | (p == 0) << 15 | blk[p - 1] << 16 | blk[p] << 24
     uint32_t word[kArr];  // then: the first match at or after x, as its record word
   };
   uint32_t rec[kArr];     // local(p) accumulator: end << 19 | end << 9 | dist (end = p + len)
@@ -478,8 +478,8 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
   // chain strictly decreases, and a walk that stops at the first link not
   // below the current one ends on any input -- even on a corrupted head.
   // Entry (byte offsets 4 p):  link (bits 0..10) | p == 0 (bit 15) |
-  // preceding byte (16..23) | tag (24..31, hash bits 16..23; within a bucket
-  // only bits 16..21 can differ).  Entries are written by ds_write_addtid_b32
+  // preceding byte (16..23) | tag (24..31: the position's own byte, which
+  // equal 4-grams share).  Entries are written by ds_write_addtid_b32
   // (2 LDS cycles per round instead of 4-6 for a strided store).
   PROF_DECL;
   const bool search = LZ4R_VARIANT != 1 && LZ4R_VARIANT != 2;
@@ -504,19 +504,21 @@ __device__ __forceinline__ int encode_block(TileLds &S, int n_arg, const uint8_t
       const uint32_t w1 = bw[16 * r], w2 = bw[16 * r + 1];
       key[r] = __builtin_amdgcn_alignbyte(w2, w1, sh);
       const uint32_t hv = key[r] * 2654435761u;                    // bucket = top 10 bits
+      // [0, 0, blk[p - 1], blk[p]]: the entry without its link.  The tag
+      // (byte 3) is the position's own first byte: any function of the 4-gram
+      // serves (equal 4-grams always agree; a pair that agrees by chance is
+      // a candidate whose lcp is < 4), and this one costs no hash bits
       if (r == 0) {
         // blk[p - 1] = byte 0 of the lane below's key (DPP wave_shr:1; lane 0
         // is p = 0, whose byte is the sentinel bit below)
         const uint32_t pb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key[0], 0x138, 0xf,
                                                                  0xf, false);
-        // [0, 0, blk[p - 1], hash bits 16..23]: the entry without its link
-        pt[0] = __builtin_amdgcn_perm(pb, hv, 0x02040C0Cu);
+        pt[0] = __builtin_amdgcn_perm(pb, key[0], 0x00040C0Cu);
       } else {
-        // rows 1..4: blk[p - 1] is byte 3 + sh of the dword pair before
-        // (one more dword in the same load, no cross-lane step)
+        // rows 1..4: bytes 3 + sh and 4 + sh of the dword pair before (one
+        // more dword in the same load, no cross-lane step)
         const uint32_t w0 = bw[16 * r - 1];
-        const uint32_t pb = __builtin_amdgcn_perm(w1, w0, 0x0C0C0C03u + sh);
-        pt[r] = __builtin_amdgcn_perm(pb, hv, 0x02040C0Cu);
+        pt[r] = __builtin_amdgcn_perm(w1, w0, 0x04030C0Cu + sh * 0x01010000u);
       }
       const int p = 64 * r + lane;
       // (full block: rounds 0..3 are all 4-gram starts)
@@ -1112,7 +1114,7 @@ __global__ __launch_bounds__(1024) void lz4_scan_partials(uint64_t *__restrict__
 //            block the u8 count + u16 size header (write_block, :415-425)
 //            land by aligned ds_or in a zeroed LDS image of the output range,
 //            and the literal runs are flattened over the lanes as aligned
-//            8-byte image words funnel-shifted out of the staged input
+//            16-byte image words funnel-shifted out of the staged input
 //   store    the image -> the stream as aligned 16-B stores (the edge chunks
 //            bytewise); nothing at or past `cap` is written.
 // This is the emission lz4_tiles used to do one block per wave; here a round
@@ -1127,7 +1129,7 @@ constexpr int kEW = 8;                               // waves per emit workgroup
 constexpr int kRecPre = kHeadW;                      // record dwords per block staged in LDS
 constexpr int kGSplit = kGT / kGH;                   // workgroups per group
 constexpr int kEmitImg = kGH * kBlkOutMax + 32;      // worst case: every block 548 B
-constexpr int kStagePad = 16;                        // literal words reach 8 B before a run
+constexpr int kStagePad = 16;                        // literal words reach 15 B before a run
 constexpr int kStage = kStagePad + kGH * kBlk + 32;  // ... and 16 B past its end
 static_assert(kStage < (1 << 16), "stage offsets fit 16 bits");
 
@@ -1150,7 +1152,7 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   __shared__ alignas(16) uint8_t img[kEmitImg];
   __shared__ alignas(16) uint8_t stage[kStage];
   __shared__ uint32_t marks[kEW][64];                // per wave: literal-run starts
-  __shared__ uint2 pmask[9];                         // pmask[k]: the low k bytes of 8 set
+  __shared__ uint4 pmask[17];                        // pmask[k]: the low k bytes of 16 set
   __shared__ uint32_t recst[kGH][kRecPre];           // each block's header + first records
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const size_t g = g_first + blockIdx.x / kGSplit;
@@ -1215,9 +1217,14 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   }
   if (hdr && g == 0 && h0 == 0 && tid == 0 && cap > 0) out[0] = (uint8_t)nb_total;
   if (tid < (h1 - h0) * kPerSlot) reinterpret_cast<uint4 *>(&recst[rhb][0])[rj] = rv;
-  if (tid < 9) {
-    const uint64_t m = tid == 8 ? ~0ull : (1ull << (8 * tid)) - 1ull;
-    pmask[tid] = make_uint2((uint32_t)m, (uint32_t)(m >> 32));
+  if (tid < 17) {
+    uint32_t m[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = min(max(tid - 4 * j, 0), 4);
+      m[j] = n == 4 ? ~0u : (1u << (8 * n)) - 1u;
+    }
+    pmask[tid] = make_uint4(m[0], m[1], m[2], m[3]);
   }
   // ---- stage: byte p of block h is stage[kStagePad + 300 (h - h0) + p] ----------
   {
@@ -1299,11 +1306,12 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
             or_bytes(out32, ib, ((bh >> 16) & 255u) | ((((bh & 0xFFFFu) + 3u) & 0xFFFFu) << 8));
           }
         }
-        // literals (LZ4.c:388), flattened over the lanes: one aligned 8-byte
-        // image word per lane and pass, funnel-shifted out of two aligned
-        // staged input words and masked to the run
+        // literals (LZ4.c:388), flattened over the lanes: one aligned 16-byte
+        // image word per lane and pass, funnel-shifted out of five aligned
+        // staged input dwords and masked to the run (16-B words: half the
+        // passes of 8-B ones; two ds_or_b64 per word)
         {
-          const int cw = valid && L > 0 ? ((ol + L - 1) >> 3) - (ol >> 3) + 1 : 0;
+          const int cw = valid && L > 0 ? ((ol + L - 1) >> 4) - (ol >> 4) + 1 : 0;
           const uint32_t cinc = wave_incl_add((uint32_t)cw);
           const int C = LZ4R_VARIANT == 31 ? 0 : (int)lane63(cinc);   // (31: tools ablation)
           const int stw = (int)dpp<0x138, 0xf, 0xf>(cinc);
@@ -1311,7 +1319,7 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
           // stage byte of that word's first image byte xs = 8 w + (src - ol), and
           // its bytes [ol, ol + L) of the image (two 16-bit fields per dword)
           const int src = kStagePad + kBlk * (hb - h0) + pend;
-          const uint32_t rw = ((uint32_t)((ol >> 3) - stw) & 0xFFFFu) | ((uint32_t)(src - ol) << 16);
+          const uint32_t rw = ((uint32_t)((ol >> 4) - stw) & 0xFFFFu) | ((uint32_t)(src - ol) << 16);
           const uint32_t rb = (uint32_t)ol | ((uint32_t)(ol + L) << 16);
           uint32_t carry = 0;                    // 1 + the last run owning a word so far
           for (int w0 = 0; w0 < C; w0 += 64) {
@@ -1326,23 +1334,21 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
             const uint32_t kw = (uint32_t)__shfl((int)rw, kr, 64);
             const uint32_t kb = (uint32_t)__shfl((int)rb, kr, 64);
             if (gw < C) {
-              const int t = 8 * ((int)(int16_t)(kw & 0xFFFFu) + gw);   // image word's first byte
+              const int t = 16 * ((int)(int16_t)(kw & 0xFFFFu) + gw);  // image word's first byte
               const int xs = t + ((int)kw >> 16);                      // its input bytes
-              // three aligned dwords and two v_alignbyte (64-bit shifts issue
-              // at ~5.6 cycles per wave-instruction, tools/valu_rate)
               const uint32_t *iw = reinterpret_cast<const uint32_t *>(stage + (xs & ~3));
-              const uint32_t d0 = iw[0], d1 = iw[1], d2 = iw[2];
+              const uint32_t d0 = iw[0], d1 = iw[1], d2 = iw[2], d3 = iw[3], d4 = iw[4];
               const uint32_t sh = (uint32_t)xs & 3u;
-              uint32_t v0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-              uint32_t v1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-              // keep the run's bytes [lb, hb) of the word: and with
-              // pmask[hb] ^ pmask[lb] (pmask[k] = the low k bytes set)
-              const int lb = max((int)(kb & 0xFFFFu) - t, 0), hb = min((int)(kb >> 16) - t, 8);
-              const uint2 ml = pmask[lb], mh = pmask[hb];
-              v0 &= ml.x ^ mh.x;
-              v1 &= ml.y ^ mh.y;
+              const int lb = max((int)(kb & 0xFFFFu) - t, 0), hb = min((int)(kb >> 16) - t, 16);
+              const uint4 ml = pmask[lb], mh = pmask[hb];
+              const uint32_t v0 = __builtin_amdgcn_alignbyte(d1, d0, sh) & (ml.x ^ mh.x);
+              const uint32_t v1 = __builtin_amdgcn_alignbyte(d2, d1, sh) & (ml.y ^ mh.y);
+              const uint32_t v2 = __builtin_amdgcn_alignbyte(d3, d2, sh) & (ml.z ^ mh.z);
+              const uint32_t v3 = __builtin_amdgcn_alignbyte(d4, d3, sh) & (ml.w ^ mh.w);
               atomicOr(reinterpret_cast<unsigned long long *>(img + t),
                        (unsigned long long)v1 << 32 | v0);
+              atomicOr(reinterpret_cast<unsigned long long *>(img + t + 8),
+                       (unsigned long long)v3 << 32 | v2);
             }
           }
         }
