@@ -1155,8 +1155,15 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   __shared__ uint4 pmask[17];                        // pmask[k]: the low k bytes of 16 set
   __shared__ uint32_t recst[kGH][kRecPre];           // each block's header + first records
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const size_t g = g_first + blockIdx.x / kGSplit;
-  const int h0 = (int)(blockIdx.x % kGSplit) * kGH;  // this workgroup: blocks [h0, h0 + kGH)
+  // XCD-aware order (workgroups b and b + 8 share an XCD): XCD b % 8 takes a
+  // contiguous eighth of the workgroups, so neighbouring outputs' boundary
+  // lines meet in one L2
+  const uint32_t nwg = (uint32_t)((ntiles - g_first * kGT + kGT - 1) / kGT) * kGSplit;
+  const uint32_t per = (nwg + 7) / 8;
+  const uint32_t wg = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  if (wg >= nwg) return;
+  const size_t g = g_first + wg / kGSplit;
+  const int h0 = (int)(wg % kGSplit) * kGH;          // this workgroup: blocks [h0, h0 + kGH)
   const size_t g0 = g * kGT;
   const int nt = (int)min((size_t)kGT, ntiles - g0);
   if (h0 >= nt) return;
@@ -1574,7 +1581,7 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
                        (uint64_t)hdr, k == 0 ? 1 : 0, k + 1 == nchunks ? 1 : 0, c->status,
                        static_cast<uint64_t *>(d_len), c->verdict);
     const size_t g0 = b0 / kGT, ng = (nbc + kGT - 1) / kGT;
-    hipExtLaunchKernelGGL(lz4_emit, dim3((unsigned)(ng * kGSplit)), dim3(64 * kEW), 0, s, nullptr,
+    hipExtLaunchKernelGGL(lz4_emit, dim3((unsigned)(8 * ((ng * kGSplit + 7) / 8))), dim3(64 * kEW), 0, s, nullptr,
                           k + 1 == nchunks ? ev(ts ? ts->c : nullptr) : nullptr, 0u, in,
                           (const uint8_t *)c->slots, (const uint8_t *)ovfs, b0,
                           (const uint32_t *)c->tsz, b1, g0, (const uint32_t *)c->gsum,
