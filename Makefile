@@ -15,6 +15,9 @@ B       := $(PKG)/build
 BIN     := $(PKG)/bin
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -ffp-contract=off -fno-strict-aliasing -fPIC -std=c++17 -Wall \
             -Wno-unused-result
+# lz4r.hip (the compressor): the max-ILP machine scheduler, -0.3 % lz4_tiles and
+# call time in three in-process A/B orders (tools/ab_inproc.py)
+LZ4R_HIPFLAGS := -mllvm -amdgpu-sched-strategy=max-ilp
 CFLAGS_HOST := -O2 -fPIC -Wall -std=gnu11 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
 LIB     := $(PKG)/lz4jpeg/liblz4jpeg.so
 HDRS    := include/lz4r.h include/jpegr.h include/lz4jpeg_compat.h include/lz4jpeg_synth.h \
@@ -36,6 +39,8 @@ $(CSRC)/jpeg_tables.h: $(CSRC)/gen_jpeg_tables.py
 $(B)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(B)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(B)/lz4r.o: HIPFLAGS += $(LZ4R_HIPFLAGS)
 
 $(B)/%.o: $(HOST)/%.c $(HDRS) $(HOST)/lzj_host.h
 	@mkdir -p $(B)

@@ -11,8 +11,9 @@ by a wait state (the round-2 hang: the first add-TID store used the previous
 block's m0 and left stale heads).
 
 Two views of the same code, both built with the product's flags:
-- the assembly of `lz4r.hip` compiled with the Makefile's own HIPFLAGS (read
-  from the Makefile, so a flag change there is a change here), where the
+- the assembly of `lz4r.hip` compiled with the Makefile's own HIPFLAGS and
+  LZ4R_HIPFLAGS (read from the Makefile, so a flag change there is a change
+  here), where the
   compiler marks the inline asm (`;;#ASMSTART`/`;;#ASMEND`);
 - the gfx950 code object extracted from the built `liblz4jpeg.so` (the bytes
   that ship), disassembled: every m0 access in it must be one of the asm
@@ -45,7 +46,7 @@ def _make_var(name):
 def asm(tmp_path_factory):
     if not os.path.exists(HIPCC):
         pytest.skip("no hipcc")
-    flags = _make_var("HIPFLAGS")
+    flags = _make_var("HIPFLAGS") + _make_var("LZ4R_HIPFLAGS")   # lz4r.o's own additions
     assert "--offload-arch=gfx950" in flags and "-fno-strict-aliasing" in flags, flags
     out = tmp_path_factory.mktemp("isa") / "lz4r.s"
     subprocess.run([HIPCC, *flags, "--cuda-device-only", "-S", SRC, "-o", str(out)],

@@ -39,8 +39,10 @@ LABEL = re.compile(r"^(\.LBB\d+_\d+):|^; (%bb\.\d+):|^\s*(1):\s*$")
 
 
 def hipflags():
-    out = subprocess.run(["make", "-s", "-C", REPO, "print-HIPFLAGS"], check=True,
-                         capture_output=True, text=True).stdout.split()
+    out = []
+    for v in ("HIPFLAGS", "LZ4R_HIPFLAGS"):        # lz4r.o's flags
+        out += subprocess.run(["make", "-s", "-C", REPO, f"print-{v}"], check=True,
+                              capture_output=True, text=True).stdout.split()
     return [f for f in out if f not in ("-fPIC",)]
 
 
