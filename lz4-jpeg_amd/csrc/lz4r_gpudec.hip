@@ -357,6 +357,92 @@ __device__ __forceinline__ int decode_block(const BytesT &p, int len, bool last,
   }
 }
 
+// The common case of decode_block, for the hot path: every token read
+// plainly (no choice points, no truncated readings), one loop iteration per
+// sequence with no data-dependent branch but the copies' own loops, so the
+// wave issues little exec-mask bookkeeping.  Returns the decoded length, or -1
+// when anything is unusual -- a reading that does not fit, or a block that
+// does not end consistently -- and decode_block then redoes the block: it
+// takes the same plain readings first and backtracks only where they fail,
+// so when this path succeeds the general one would return the same bytes.
+template <typename BytesT, typename SlotT>
+__device__ __forceinline__ int decode_block_plain(const BytesT &p, int len, bool last,
+                                                  const SlotT &o) {
+  const uint64_t h0 = p.ld8(0);
+  const int nseq = (int)(h0 & 255);
+  const int want = (int)((h0 >> 8) & 0xFFFF) - 3;    // LZ4.c:617
+  if (len < 3 || nseq == 0 || want < 0) return -1;
+  int k = 0, ip = 3, pos = 0;
+  V16 h = p.ld16(3);
+  bool bad = false;
+  while (k < nseq) {
+    // the window as dwords; bytes [o, o + 4) of it by one v_alignbyte of two
+    // selected dwords (no 64-bit shifts, no branches)
+    const uint32_t w0 = (uint32_t)h.lo, w1 = (uint32_t)(h.lo >> 32);
+    const uint32_t w2 = (uint32_t)h.hi, w3 = (uint32_t)(h.hi >> 32);
+    const int tok = (int)(w0 & 255), Sz = (int)((w0 >> 8) & 0xFFFF);
+    const int e0 = (int)(w0 >> 24), e1 = (int)(w1 & 255);
+    const int tl = tok >> 4, tm = tok & 15;
+    const int mx = tm == 15 ? 1 : 0;
+    const bool big = tl == 15;
+    // the plain reading as selects and lane masks, not branches
+    const bool ff = e0 == 255;
+    const int le = (big ? 1 : 0) + ((big & ff) ? 1 : 0);
+    const int Lb = Sz - 5 - le - mx;
+    const int L = big ? Lb : tl;
+    const int r = (L - 15) & 255;
+    const bool okb = (L >= 15) & ((ff & (r == 255) & (e1 == 0)) | (!ff & (r == e0)));
+    const bool oks = Sz == L + 5 + mx;
+    bool okp = (big & okb) | (!big & oks);
+    const int lit = ip + 3 + le;
+    okp = okp && ip + 3 <= len && ip - 3 + Sz <= want && lit + L + 2 <= len && pos + L <= kBlk;
+    const int nip = lit + L + 2 + mx;
+    const V16 hn = p.ld16(okp ? nip : ip);           // next window, in flight during the copies
+    const int off = lit + L - ip;                    // distance bytes within the window?
+    uint32_t t;
+    {
+      const int wi = off >> 2;
+      const uint32_t a = wi == 0 ? w0 : wi == 1 ? w1 : wi == 2 ? w2 : w3;
+      const uint32_t c = wi == 0 ? w1 : wi == 1 ? w2 : w3;
+      t = __builtin_amdgcn_alignbyte(c, a, (uint32_t)off & 3u);
+    }
+    if (off + 3 > 16) t = (uint32_t)p.ld8(okp ? lit + L : 0);
+    const int D = (int)(t & 0xFFFF);
+    const bool hasm = D != 0;
+    const int M = hasm ? (mx ? 19 + (int)((t >> 16) & 255) : tm + 4) : 0;
+    okp = okp && (hasm ? (nip <= len && D <= pos + L && pos + L + M <= kBlk)
+                       : (k + 1 == nseq && tm == 0));   // literal-only tail, LZ4.c:585-613
+    if (!okp) {
+      bad = true;
+      break;
+    }
+    // literals: the window's bytes, then 16 at a time from the stream
+    const int wl = min(L, ip + 16 - lit);
+    if (wl > 0) {
+      // the window from byte d = lit - ip (3, 4 or 5): dwords from w[d >> 2]
+      const bool d4 = le > 0;                         // d = 3 + le
+      const uint32_t sh = (uint32_t)(3 + le) & 3u;
+      const uint32_t s0 = d4 ? w1 : w0, s1 = d4 ? w2 : w1, s2 = d4 ? w3 : w2, s3 = d4 ? 0u : w3;
+      const uint32_t o0 = __builtin_amdgcn_alignbyte(s1, s0, sh);
+      const uint32_t o1 = __builtin_amdgcn_alignbyte(s2, s1, sh);
+      const uint32_t o2 = __builtin_amdgcn_alignbyte(s3, s2, sh);
+      const uint32_t o3 = __builtin_amdgcn_alignbyte(0u, s3, sh);
+      o.st_fast(pos, {(uint64_t)o1 << 32 | o0, (uint64_t)o3 << 32 | o2}, wl);
+    }
+    for (int i = wl; i < L; i += 16) o.st_fast(pos + i, p.ld16(lit + i), min(16, L - i));
+    // match: one 16-B piece when it neither overlaps itself nor exceeds 16
+    const int q = pos + L;
+    if (M > 0 && M <= 16 && D >= 16) o.st_fast(q, o.ld16(q - D), M);
+    else if (M > 0) copy_match(o, q, D, M);
+    ++k;
+    ip = nip;
+    h = hn;
+    pos += L + M;
+  }
+  if (bad || ip != len || ip - 3 != want || !(pos == kBlk || (last && pos >= 1))) return -1;
+  return pos;
+}
+
 // nb_dev (bare streams): the block count is read on the device, the grid is
 // sized for an upper bound, and nothing is decoded unless *gate is 0
 __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
@@ -404,10 +490,13 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
       // monotone; only the stream's last few blocks take the checked path)
       // (compressor offsets are monotone: the wave's blocks lie within
       // 32 x kInMax bytes of its base; other offsets take the checked path)
-      if (beg + (size_t)kInMax + 64 <= in_len && beg >= wbeg && beg - wbeg < (1u << 30))
-        q = decode_block(BytesW{wbase, (uint32_t)(beg - wbeg)}, (int)(end - beg), last, o);
-      else
+      if (beg + (size_t)kInMax + 64 <= in_len && beg >= wbeg && beg - wbeg < (1u << 30)) {
+        const BytesW bw{wbase, (uint32_t)(beg - wbeg)};
+        q = decode_block_plain(bw, (int)(end - beg), last, o);
+        if (q < 0) q = decode_block(bw, (int)(end - beg), last, o);
+      } else {
         q = decode_block(Bytes<true>{in + beg, in_len - beg}, (int)(end - beg), last, o);
+      }
     }
     if (q == 0) atomicMin(&result[1], (unsigned long long)b + 1);
     else if (last) result[0] = (unsigned long long)(b * kBlk + q);

@@ -46,11 +46,11 @@ def hipflags():
     return [f for f in out if f not in ("-fPIC",)]
 
 
-def compile_asm(src, extra=()):
+def compile_asm(src, extra=(), flags=None):
     os.makedirs(OUT, exist_ok=True)
     s = os.path.join(OUT, "bb_src.s")
-    subprocess.run(["/opt/rocm/bin/hipcc", *hipflags(), *extra, "--cuda-device-only", "-S", src,
-                    "-o", s], check=True, stderr=subprocess.DEVNULL)
+    subprocess.run(["/opt/rocm/bin/hipcc", *(flags or hipflags()), *extra, "--cuda-device-only",
+                    "-S", src, "-o", s], check=True, stderr=subprocess.DEVNULL)
     return open(s).read().splitlines()
 
 
@@ -98,6 +98,26 @@ PROLOGUE = ["\ts_getpc_b64 s[{s}:{s1}]",
             "\tv_mov_b32 v{v2}, 1"]
 
 
+# a kernel with no free SGPR pair (lz4_decode_blocks uses s0..s98): EXEC saved
+# in two lanes of a spare VGPR, the prologue's PC in VCC (unset at entry)
+BUMP_V = ["\tv_writelane_b32 v{v3}, vcc_lo, 0",      # VCC parked in a spare VGPR,
+          "\tv_writelane_b32 v{v3}, vcc_hi, 1",      # EXEC parked in VCC
+          "\ts_mov_b64 vcc, exec",
+          "\ts_mov_b64 exec, 1",
+          "\ts_nop 1",
+          "\tglobal_atomic_add v[{v}:{v1}], v{v2}, off offset:{off}",
+          "\ts_mov_b64 exec, vcc",
+          "\tv_readlane_b32 vcc_lo, v{v3}, 0",
+          "\tv_readlane_b32 vcc_hi, v{v3}, 1",
+          "\ts_nop 5"]
+PROLOGUE_V = ["\ts_getpc_b64 vcc",
+              "\ts_add_u32 vcc_lo, vcc_lo, lz4r_bb_acc@rel32@lo+4",
+              "\ts_addc_u32 vcc_hi, vcc_hi, lz4r_bb_acc@rel32@hi+12",
+              "\tv_mov_b32 v{v}, vcc_lo",
+              "\tv_mov_b32 v{v1}, vcc_hi",
+              "\tv_mov_b32 v{v2}, 1"]
+
+
 def instrument(L, st, en, kname):
     body = L[st:en]
     used = set()
@@ -113,17 +133,19 @@ def instrument(L, st, en, kname):
             used.add(("s", int(r)))
     vb = (max(k for t, k in used if t == "v") + 2) & ~1
     sb = (max(k for t, k in used if t == "s") + 2) & ~1
-    R = dict(v=vb, v1=vb + 1, v2=vb + 2, s=sb, s1=sb + 1)
-    assert vb + 3 <= 256 and sb + 2 <= 100
-    out = list(L[:st + 1]) + [x.format(**R) for x in PROLOGUE]
+    R = dict(v=vb, v1=vb + 1, v2=vb + 2, v3=vb + 3, s=sb, s1=sb + 1)
+    vmode = sb + 2 > 100                                  # no free SGPR pair
+    assert vb + 4 <= 256
+    bump, pro = (BUMP_V, PROLOGUE_V) if vmode else (BUMP, PROLOGUE)
+    out = list(L[:st + 1]) + [x.format(**R) for x in pro]
     k = 0
     off = lambda k: f"{4 * k}"
-    out += [b.format(off=off(k), **R) for b in BUMP]      # entry block
+    out += [b.format(off=off(k), **R) for b in bump]      # entry block
     k += 1
     for i in range(st + 1, en):
         out.append(L[i])
         if LABEL.match(L[i]):
-            out += [b.format(off=off(k), **R) for b in BUMP]
+            out += [b.format(off=off(k), **R) for b in bump]
             k += 1
     assert k <= NCNT and 4 * k < 4096
     out += L[en:]
@@ -133,8 +155,9 @@ def instrument(L, st, en, kname):
                  rf"\g<1>{(vb + 4 + 3) & ~3}", txt)
     txt = re.sub(r"(\.amdhsa_kernel " + kname + r"\n(?:.*\n)*?\s*\.amdhsa_accum_offset )\d+",
                  rf"\g<1>{(vb + 4 + 3) & ~3}", txt)
-    txt = re.sub(r"(\.amdhsa_kernel " + kname + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_sgpr )\d+",
-                 rf"\g<1>{sb + 2}", txt)
+    if not vmode:
+        txt = re.sub(r"(\.amdhsa_kernel " + kname + r"\n(?:.*\n)*?\s*\.amdhsa_next_free_sgpr )\d+",
+                     rf"\g<1>{sb + 2}", txt)
     txt += ("\n\t.type\tlz4r_bb_acc,@object\n\t.section\t.bss.lz4r_bb_acc,\"aw\",@nobits\n"
             "\t.globl\tlz4r_bb_acc\n\t.protected\tlz4r_bb_acc\n\t.p2align\t8\nlz4r_bb_acc:\n\t.zero\t4096\n"
             "\t.size\tlz4r_bb_acc, 4096\n")
@@ -142,14 +165,30 @@ def instrument(L, st, en, kname):
 
 
 EMIT = "_ZN12_GLOBAL__N_18lz4_emit"
+DEC = "_ZN12_GLOBAL__N_117lz4_decode_blocks"
+
+
+def dec_flags():
+    """lz4r_gpudec.o's flags: HIPFLAGS + its scheduler (the Makefile's target rule)."""
+    base = subprocess.run(["make", "-s", "-C", REPO, "print-HIPFLAGS"], check=True,
+                          capture_output=True, text=True).stdout.split()
+    mk = open(os.path.join(REPO, "Makefile")).read()
+    m = re.search(r"^\$\(B\)/lz4r_gpudec\.o: HIPFLAGS \+= (.*)$", mk, re.M)
+    return [f for f in base if f != "-fPIC"] + (m.group(1).split() if m else [])
 
 
 def build(src=None, name="prod", kernel=KERNEL):
-    """kernel: KERNEL (lz4_tiles<true>) or EMIT (lz4_emit; name gets an "emit_" prefix)."""
-    src = src or os.path.join(REPO, "lz4-jpeg_amd", "csrc", "lz4r.hip")
-    if kernel == EMIT:
-        name = "emit_" + name
-    L = compile_asm(src)
+    """kernel: KERNEL (lz4_tiles<true>), EMIT (lz4_emit; name gets an "emit_"
+    prefix) or DEC (lz4_decode_blocks of lz4r_gpudec.hip; "dec_")."""
+    if kernel == DEC:
+        src = src or os.path.join(REPO, "lz4-jpeg_amd", "csrc", "lz4r_gpudec.hip")
+        name = "dec_" + name
+        L = compile_asm(src, ("-I", os.path.join(REPO, "include")), flags=dec_flags())
+    else:
+        src = src or os.path.join(REPO, "lz4-jpeg_amd", "csrc", "lz4r.hip")
+        if kernel == EMIT:
+            name = "emit_" + name
+        L = compile_asm(src)
     st, en = kernel_range(L, kernel)
     bbs = basic_blocks(L, st, en)
     kname = L[st].split(":")[0]
@@ -388,9 +427,54 @@ def report(countsf, staticf, costf=None, pmcf=None, clock_ghz=None, ms_per_gib=N
     return out
 
 
+def run_dec(outdir, name="prod", nbytes=1 << 30):
+    """The instrumented lz4_decode_blocks from the module over the product's
+    compressed bench corpus (the compressor's device block offsets); the
+    output must equal the input."""
+    sys.path.insert(0, os.path.join(REPO, "lz4-jpeg_amd"))
+    import torch
+    from lz4jpeg import lz4, synth
+    hip = ctypes.CDLL("libamdhip64.so")
+    torch.cuda.init()
+    n = nbytes
+    d_in = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    synth.random_passages_device(d_in, n, length=30000, seed=1, first=0)
+    comp = lz4.Compressor()
+    d_stream, length = comp.compress_device(d_in, n)
+    offs, nb = comp.block_offsets_device()
+    out = torch.zeros(n + 300, dtype=torch.uint8, device="cuda")
+    res = torch.tensor([0, -1], dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    mod = ctypes.c_void_p()
+    assert hip.hipModuleLoad(ctypes.byref(mod), os.path.join(OUT, f"bbcnt_dec_{name}.co").encode()) == 0
+    S = json.load(open(os.path.join(OUT, f"bb_static_dec_{name}.json")))
+    f = ctypes.c_void_p()
+    assert hip.hipModuleGetFunction(ctypes.byref(f), mod, S["kernel"].encode()) == 0
+    acc, accsz = ctypes.c_void_p(), ctypes.c_size_t()
+    assert hip.hipModuleGetGlobal(ctypes.byref(acc), ctypes.byref(accsz), mod, b"lz4r_bb_acc") == 0
+    assert hip.hipMemset(acc, 0, ctypes.c_size_t(4 * NCNT)) == 0
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    U64 = ctypes.c_uint64
+    grid = (nb + 31) // 32
+    _launch(hip, f, grid, 64, [P(d_stream), U64(length), ctypes.c_void_p(offs), U64(nb), P(out),
+                               U64(n + 300), P(res), ctypes.c_void_p(0), ctypes.c_void_p(0)])
+    assert hip.hipDeviceSynchronize() == 0
+    host = (ctypes.c_uint32 * NCNT)()
+    assert hip.hipMemcpy(host, acc, ctypes.c_size_t(4 * NCNT), 2) == 0
+    same = bool(torch.equal(out[:n], d_in[:n])) and int(res[0].item()) == n
+    os.makedirs(outdir, exist_ok=True)
+    r = {"bytes": n, "blocks": nb, "waves": grid, "output_equal_input": same, "counts": list(host)}
+    json.dump(r, open(os.path.join(outdir, f"bbcounts_dec_{name}.json"), "w"))
+    print(json.dumps({k: v for k, v in r.items() if k != "counts"}))
+
+
 if __name__ == "__main__":
     cmd = sys.argv[1]
-    if cmd == "build":              # build [src.hip name]
+    if cmd == "build_dec":
+        build(*(sys.argv[2:4] or [None, "prod"]), kernel=DEC)
+    elif cmd == "run_dec":
+        run_dec(sys.argv[2], *sys.argv[3:4])
+    elif cmd == "build":              # build [src.hip name]
         build(*sys.argv[2:4])
     elif cmd == "build_emit":       # build_emit [src.hip name]
         build(*(sys.argv[2:4] or [None, "prod"]), kernel=EMIT)
