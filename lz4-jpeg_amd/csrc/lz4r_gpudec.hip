@@ -71,8 +71,14 @@ typedef uint64_t u64u __attribute__((aligned(1)));
 typedef uint32_t u32u __attribute__((aligned(1)));
 typedef uint16_t u16u __attribute__((aligned(1)));
 
+// Slots kSlotS apart: 300 bytes of output and 16 of slack, so a 16-B store
+// that starts inside the block never reaches the next lane's slot (no
+// exact-size stores at the slot end).
+constexpr int kSlotS = kBlk + 16;
+
 struct DecLds {
-  alignas(16) uint8_t out[kBPW * kBlk + 32];     // lane l's block at out[300 l] (+ slack)
+  alignas(16) uint8_t out[kBPW * kSlotS + 48];  // lane l's block at out[kSlotS l] (+ slack)
+  uint4 sel[17];                                 // sel[k]: v_perm selectors, bytes < k from A
   uint32_t qlen[kLanes];                         // decoded bytes per block (0 = failed)
 };
 
@@ -171,6 +177,23 @@ struct Slot {
       w >>= 16;
     }
     if (n & 1) o[a] = (uint8_t)w;
+  }
+};
+
+// The output slot of the fast path: every store is a whole 16-B store (the
+// slot's 16-B slack takes what passes its 300 bytes).
+struct SlotW {
+  uint8_t *o;
+  __device__ __forceinline__ uint64_t ld8(int a) const {
+    return *reinterpret_cast<const u64u *>(o + a);
+  }
+  __device__ __forceinline__ V16 ld16(int a) const {
+    const u64u *q = reinterpret_cast<const u64u *>(o + a);
+    return {q[0], q[1]};
+  }
+  __device__ __forceinline__ void st_fast(int a, V16 v, int) const {
+    *reinterpret_cast<u64u *>(o + a) = v.lo;
+    *reinterpret_cast<u64u *>(o + a + 8) = v.hi;
   }
 };
 
@@ -471,7 +494,7 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
     const size_t beg = 1 + boff[b];
     const size_t end = last ? in_len : 1 + boff[b + 1];
     if (end >= beg + 3 && end <= in_len && end - beg <= (size_t)kInMax) {
-      const Slot o{S.out + lane * kBlk};
+      const Slot o{S.out + lane * kSlotS};
       // touch the block's next four 128-B lines now: the walk's header loads
       // then hit L2 instead of waiting on HBM one line at a time (the values
       // are folded into pfx after the walk; 1.82 -> 1.66 ms per GiB)
@@ -492,7 +515,7 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
       // 32 x kInMax bytes of its base; other offsets take the checked path)
       if (beg + (size_t)kInMax + 64 <= in_len && beg >= wbeg && beg - wbeg < (1u << 30)) {
         const BytesW bw{wbase, (uint32_t)(beg - wbeg)};
-        q = decode_block_plain(bw, (int)(end - beg), last, o);
+        q = decode_block_plain(bw, (int)(end - beg), last, SlotW{S.out + lane * kSlotS});
         if (q < 0) q = decode_block(bw, (int)(end - beg), last, o);
       } else {
         q = decode_block(Bytes<true>{in + beg, in_len - beg}, (int)(end - beg), last, o);
@@ -507,28 +530,56 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
   for (int t = 0; t < kPfN; ++t) pfx ^= pfv[t];
   if (pfx == 0x5A5A5A5Au && q == 1000) q = 0;
   S.qlen[lane] = (uint32_t)q;
+  if (lane < 17) {                                   // sel[k]: dword j, byte m from A iff 4 j + m < k
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) x |= (uint32_t)(4 * j + m < lane ? m : 4 + m) << (8 * m);
+      w[j] = x;
+    }
+    S.sel[lane] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
   __syncthreads();
 
   // ---- store the wave's contiguous output -----------------------------------
   // every block but the last decodes to exactly 300 bytes, so the valid range
-  // is [300 b0, 300 b0 + sum q); a failed block leaves garbage (error raised)
+  // is [300 b0, 300 b0 + sum q); a failed block leaves garbage (error raised).
+  // Output byte x is slot l = x / 300, byte x - 300 l; a 16-B chunk that
+  // crosses a slot end takes its first k bytes from slot l (A) and the rest
+  // from slot l + 1, 16 B further on (B): one v_perm per dword.
   size_t total = 0;
   for (int l = 0; l < nl; ++l) total += l + 1 < nl ? kBlk : S.qlen[l];
   const size_t o0 = b0 * (size_t)kBlk;
   if (o0 >= out_cap) return;
   if (o0 + total > out_cap) total = out_cap - o0;
+  auto src_of = [](uint32_t x) {                     // LDS offset of output byte x (< 2^15)
+    const uint32_t l = (x * 27963u) >> 23;           // x / 300
+    return x + 16u * l;
+  };
   if (((reinterpret_cast<uintptr_t>(out) + o0) & 15) == 0) {
     const int nv = (int)(total >> 4);
-    const uint4 *src = reinterpret_cast<const uint4 *>(S.out);
     uint4 *dst = reinterpret_cast<uint4 *>(out + o0);
-    // written once: non-temporal 16-B stores (-1.3 %, tools/ab_dec_inproc.py)
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    for (int v = lane; v < nv; v += kLanes)
-      __builtin_nontemporal_store(reinterpret_cast<const u32x4 *>(src)[v],
-                                  reinterpret_cast<u32x4 *>(dst) + v);
-    for (size_t i = (size_t)nv * 16 + lane; i < total; i += kLanes) out[o0 + i] = S.out[i];
+    for (int v = lane; v < nv; v += kLanes) {
+      const uint32_t x = 16u * (uint32_t)v;
+      const uint32_t l = (x * 27963u) >> 23;
+      const uint32_t off = x - 300u * l;
+      const uint32_t k = min(300u - off, 16u);
+      const uint8_t *a = S.out + x + 16u * l;
+      const uint4 A = *reinterpret_cast<const uint4 *>(a);
+      const uint4 B = *reinterpret_cast<const uint4 *>(a + 16);
+      const uint4 sl = S.sel[k];
+      const u32x4 m = {__builtin_amdgcn_perm(B.x, A.x, sl.x), __builtin_amdgcn_perm(B.y, A.y, sl.y),
+                       __builtin_amdgcn_perm(B.z, A.z, sl.z), __builtin_amdgcn_perm(B.w, A.w, sl.w)};
+      // written once: non-temporal 16-B stores (-1.3 %, tools/ab_dec_inproc.py)
+      __builtin_nontemporal_store(m, reinterpret_cast<u32x4 *>(dst) + v);
+    }
+    for (size_t i = (size_t)nv * 16 + lane; i < total; i += kLanes)
+      out[o0 + i] = S.out[src_of((uint32_t)i)];
   } else {
-    for (size_t i = lane; i < total; i += kLanes) out[o0 + i] = S.out[i];
+    for (size_t i = lane; i < total; i += kLanes) out[o0 + i] = S.out[src_of((uint32_t)i)];
   }
 }
 
