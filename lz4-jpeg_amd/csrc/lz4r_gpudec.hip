@@ -268,17 +268,19 @@ __device__ __forceinline__ void copy_match(const SlotT &o, int q, int D, int M) 
   int i = 0, d = D;
   if (D < 8) {                                   // seed: whole periods within 8 bytes
     const uint64_t x = replicate(o.ld8(q - D), D);
-    const int per = 8 - 8 % D;
+    const int per = (int)((0x76586880u >> (4 * D)) & 15u);   // 8 - 8 % D, nibble D
     i = M < per ? M : per;
     o.st_fast(q, {x, x}, i);
-    d = i + D - i % D;                           // multiple of D, <= i + D
+    d = i + D;                                   // i is a multiple of D (or M: done)
   }
+  // while d < 16 every step copies d bytes, so i stays a multiple of D and the
+  // next distance is i + D (no modulo); from d >= 16 on, d no longer changes
   while (i < M) {
     int n = M - i < 16 ? M - i : 16;
     if (n > d) n = d;
     o.st_fast(q + i, o.ld16(q + i - d), n);
     i += n;
-    if (d < 16) d = i + D - i % D;               // grow while short
+    if (d < 16) d = i + D;                       // grow while short
   }
 }
 
