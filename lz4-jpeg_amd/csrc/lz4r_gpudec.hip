@@ -11,25 +11,28 @@
 //
 // Mapping: one LANE per block, 32 consecutive blocks per wave (a wave per
 // block would issue every serial parsing step as a full wave instruction).
-// The walk is latency- and issue-bound, so the kernel keeps LDS small for
-// occupancy (9.6 KB of LDS per wave: the 32 output slots; 16 waves/CU) and
-// keeps instruction counts low:
+// The walk is issue-bound (the divergent per-lane loop), so the kernel keeps
+// LDS small for occupancy (10.1 KB per wave: 32 output slots of 300 B + 16 B
+// of slack; 15 waves/CU) and the loop free of exec-mask bookkeeping:
+//   - every block first goes through decode_block_plain: every token read
+//     plainly, the header decoded as selects and lane masks, the window's
+//     bytes by v_alignbyte of selected dwords, whole 16-B stores only (the
+//     slot's slack takes what passes its end); anything unusual (a reading
+//     that does not fit, an inconsistent end) returns -1 and the general
+//     decode_block below redoes the block;
 //   - the lane reads its encoded bytes with single unaligned 8/16-byte
 //     global loads (L1/L2 absorb the re-reads of the wave's ~20 KB range),
 //     after touching the block's next four 128-B lines up front so that the
 //     serial walk does not wait on HBM once per line;
-//   - a sequence header is decoded branch-free for the plain reading; the
-//     rare truncated readings (below) take a separate path;
 //   - literals move in 16-byte chunks; a match of distance D is copied in
 //     chunks of min(16, d) bytes at a distance d that grows from D (the
 //     match is D-periodic, so any multiple of D up to the bytes already
 //     written + D is a valid distance), with D < 8 seeded by replicating
 //     its period over 8 bytes;
-//   - stores into the LDS slot are unaligned 16-byte stores (the hardware
-//     runs in unaligned mode) whose bytes past the wanted ones fall beyond
-//     the lane's write frontier; within 16 bytes of the slot end they are
-//     exact-size (b64/b32/b16/b8 pieces), so no lane touches a neighbour;
-//   - the wave's 32 x 300 = 9600 contiguous bytes leave as 16-B stores.
+//   - the general path's stores within 16 bytes of the 300-B end are
+//     exact-size (b64/b32/b16/b8 pieces);
+//   - the wave's 32 x 300 = 9600 contiguous output bytes leave as 16-B
+//     stores gathered across the slot ends (one v_perm per dword).
 // Measured alternatives that lost (1 GiB text, MI355X): one wave per block
 // (15.5 ms), nested copy loops with byte stores (3.4 ms), staging the wave's
 // input in LDS (halves occupancy: 2x slower), output slots in global memory

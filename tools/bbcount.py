@@ -166,6 +166,7 @@ def instrument(L, st, en, kname):
 
 EMIT = "_ZN12_GLOBAL__N_18lz4_emit"
 DEC = "_ZN12_GLOBAL__N_117lz4_decode_blocks"
+ENC = "_ZN12_GLOBAL__N_119entropy_encode_laneILb"   # + "1EE" (luma) / "0EE" (chroma)
 
 
 def dec_flags():
@@ -184,6 +185,13 @@ def build(src=None, name="prod", kernel=KERNEL):
         src = src or os.path.join(REPO, "lz4-jpeg_amd", "csrc", "lz4r_gpudec.hip")
         name = "dec_" + name
         L = compile_asm(src, ("-I", os.path.join(REPO, "include")), flags=dec_flags())
+    elif kernel.startswith(ENC):
+        src = src or os.path.join(REPO, "lz4-jpeg_amd", "csrc", "jpegr_entropy.hip")
+        name = ("enc1_" if kernel.endswith("1EE") else "enc0_") + name
+        base = subprocess.run(["make", "-s", "-C", REPO, "print-HIPFLAGS"], check=True,
+                              capture_output=True, text=True).stdout.split()
+        L = compile_asm(src, ("-I", os.path.join(REPO, "include")),
+                        flags=[f for f in base if f != "-fPIC"])
     else:
         src = src or os.path.join(REPO, "lz4-jpeg_amd", "csrc", "lz4r.hip")
         if kernel == EMIT:
@@ -468,9 +476,60 @@ def run_dec(outdir, name="prod", nbytes=1 << 30):
     print(json.dumps({k: v for k, v in r.items() if k != "counts"}))
 
 
+def run_enc(outdir, name="prod", luma="1"):
+    """The instrumented entropy_encode_lane<luma> from the module over a 4K
+    random image's coefficients (the product's encode_device); its bits,
+    meta and table of that channel must equal the product's."""
+    sys.path.insert(0, os.path.join(REPO, "lz4-jpeg_amd"))
+    import torch
+    from lz4jpeg import jpeg, synth
+    hip = ctypes.CDLL("libamdhip64.so")
+    torch.cuda.init()
+    W, H = 3840, 2160
+    d_img = torch.from_numpy(synth.rand_rgba(W, H, seed=1)).cuda()
+    d_coef = jpeg.encode_device(d_img, W, H)
+    nt = jpeg.tiles(W, H)
+    ref = jpeg.Entropy(nt)
+    ref.encode(d_coef)
+    mine = jpeg.Entropy(nt)
+    mine.scratch.zero_()
+    torch.cuda.synchronize()
+    tag = "enc1_" if luma == "1" else "enc0_"
+    mod = ctypes.c_void_p()
+    assert hip.hipModuleLoad(ctypes.byref(mod), os.path.join(OUT, f"bbcnt_{tag}{name}.co").encode()) == 0
+    S = json.load(open(os.path.join(OUT, f"bb_static_{tag}{name}.json")))
+    f = ctypes.c_void_p()
+    assert hip.hipModuleGetFunction(ctypes.byref(f), mod, S["kernel"].encode()) == 0
+    acc, accsz = ctypes.c_void_p(), ctypes.c_size_t()
+    assert hip.hipModuleGetGlobal(ctypes.byref(acc), ctypes.byref(accsz), mod, b"lz4r_bb_acc") == 0
+    assert hip.hipMemset(acc, 0, ctypes.c_size_t(4 * NCNT)) == 0
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    groups = (nt + 63) // 64 * (1 if luma == "1" else 2)
+    deferred = ctypes.c_void_p(mine.scratch.data_ptr() + 256)
+    _launch(hip, f, groups, 64, [P(d_coef), ctypes.c_uint64(nt), P(mine.bits), P(mine.meta),
+                                 P(mine.table), P(mine.scratch), deferred, P(mine.status)])
+    assert hip.hipDeviceSynchronize() == 0
+    host = (ctypes.c_uint32 * NCNT)()
+    assert hip.hipMemcpy(host, acc, ctypes.c_size_t(4 * NCNT), 2) == 0
+    cs = [0] if luma == "1" else [1, 2]
+    same = True
+    for c in cs:
+        off, n = (0, 128) if c == 0 else ((128, 64) if c == 1 else (192, 64))
+        same &= bool(torch.equal(mine.meta.view(nt, 3)[:, c], ref.meta.view(nt, 3)[:, c]))
+        same &= bool(torch.equal(mine.bits.view(nt, 256)[:, off:off + n], ref.bits.view(nt, 256)[:, off:off + n]))
+    os.makedirs(outdir, exist_ok=True)
+    r = {"tiles": nt, "waves": groups, "channel_equal_product": same, "counts": list(host)}
+    json.dump(r, open(os.path.join(outdir, f"bbcounts_{tag}{name}.json"), "w"))
+    print(json.dumps({k: v for k, v in r.items() if k != "counts"}))
+
+
 if __name__ == "__main__":
     cmd = sys.argv[1]
-    if cmd == "build_dec":
+    if cmd == "build_enc":          # build_enc 1|0 [src.hip name]
+        build(*(sys.argv[3:5] or [None, "prod"]), kernel=ENC + sys.argv[2] + "EE")
+    elif cmd == "run_enc":          # run_enc outdir 1|0 [name]
+        run_enc(sys.argv[2], *(sys.argv[4:5] or ["prod"]), luma=sys.argv[3])
+    elif cmd == "build_dec":
         build(*(sys.argv[2:4] or [None, "prod"]), kernel=DEC)
     elif cmd == "run_dec":
         run_dec(sys.argv[2], *sys.argv[3:4])
