@@ -172,7 +172,8 @@ __device__ __forceinline__ uint16_t sift(const W &w, int size, int i, uint16_t x
 // levels rewrite x at its index (idempotent).  The loop form above paid the
 // exec-mask bookkeeping of every lane's own exit at every level.
 template <int Cap, int kDepth, class W>
-__device__ __forceinline__ uint16_t sift_depth(const W &w, int size, int i, uint16_t x) {
+__device__ __forceinline__ uint16_t sift_depth(const W &w, int size, int i, uint16_t x,
+                                               int *fi = nullptr) {
   constexpr int kMaxSlot = Cap & ~1;
   static_assert(Cap <= 31 && kDepth >= 1 && kDepth <= 4, "fixed depth");
   // counts compare as whole entries against a count with a zero id byte
@@ -212,6 +213,7 @@ __device__ __forceinline__ uint16_t sift_depth(const W &w, int size, int i, uint
     }
   }
   w.heap[i + 1] = x;
+  if (fi) *fi = i;                                    // where x landed
   return top;
 }
 
@@ -224,22 +226,32 @@ __device__ __forceinline__ uint16_t sift_fixed(const W &w, int size, int i, uint
 // The same with the depth cut to what a wave-uniform bound allows: no lane
 // of the wave sifts more than `levels` levels (a uniform branch picks the
 // unrolled depth).
-template <int Cap, class W>
-__device__ __forceinline__ uint16_t sift_levels(const W &w, int levels, int size, int i,
-                                                uint16_t x) {
-  if constexpr (Cap >= 16) {
-    if (levels >= 4) return sift_depth<Cap, 4>(w, size, i, x);
-  }
-  if (levels >= 3) return sift_depth<Cap, 3>(w, size, i, x);
-  if (levels == 2) return sift_depth<Cap, 2>(w, size, i, x);
-  return sift_depth<Cap, 1>(w, size, i, x);
-}
-
 // levels a sift from index i can descend in a heap of at most s entries
-__device__ __forceinline__ int sift_levels_bound(int s, int i) {
+__host__ __device__ constexpr int sift_levels_bound(int s, int i) {
   int d = 0;
   for (int j = i; 2 * j + 1 < s; j = 2 * j + 1) ++d;
   return d;
+}
+
+// build_heap's sifts (JPEG.c:913-936) from index I down to 0, unrolled so
+// that each sift's x is the entry's initial value from registers: a sift
+// from a later index moves only entries of that index's subtree, which holds
+// no earlier index.  Returns, through root, the entry left at index 0.
+template <int Cap, int I, class W>
+__device__ __forceinline__ void build_heap_from(const W &w, int umax, int U,
+                                                const uint32_t *h0, uint16_t &root) {
+  if constexpr (I >= 0) {
+    if (I < umax / 2) {                                 // uniform
+      if (I < U / 2) {
+        // the depth of index I in a heap of Cap: the levels of the wave's
+        // own heaps (umax) are the same for all but small streams
+        const uint16_t t =
+            sift_depth<Cap, sift_levels_bound(Cap, I)>(w, U, I, (uint16_t)h0[I]);
+        if (I == 0) root = t;
+      }
+    }
+    build_heap_from<Cap, I - 1>(w, umax, U, h0, root);
+  }
 }
 
 template <int Cap, class W>
@@ -255,8 +267,10 @@ __device__ __forceinline__ uint16_t sift_any(const W &w, int size, int i, uint16
 // first).  In: w.heap[u + 1] = count << 8 | u and w.sym[u] for u < U.  Out:
 // w.code / w.len per leaf and the table (value | length << 16 per code, DFS
 // order).  Returns true when a code exceeds the reference's char code[32].
+// h0 (Cap <= 31): heap entry i's initial value (count << 8 | i) for i < U.
 template <int Cap, class W>
-__device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
+__device__ __forceinline__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table,
+                                           const uint32_t *h0 = nullptr) {
   int size = U, next = U;
   uint16_t root;
   int umax = 0;
@@ -268,22 +282,33 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
 #pragma unroll
     for (int b = 4; b >= 0; --b)
       if (__ballot(U >= (umax | (1 << b)))) umax |= 1 << b;
-    for (int i = umax / 2 - 1; i >= 0; --i) {
-      const int lv = sift_levels_bound(umax, i);
-      if (i < U / 2) sift_levels<Cap>(w, lv, U, i, w.heap[i + 1]);
-    }
-    root = w.heap[1];
-    for (int t = 0; umax - t > 1; ++t) {
-      const int l1 = sift_levels_bound(umax - t - 1, 0), l2 = sift_levels_bound(umax - t - 2, 0);
+    root = (uint16_t)h0[0];
+    build_heap_from<Cap, Cap / 2 - 1>(w, umax, U, h0, root);
+    // Each pop moves the last entry to the root and sifts it.  The first pop's
+    // last entry is the node the previous merge appended (in registers); the
+    // second pop's is read before the first sift, which changes that index
+    // (the heap's last: no children) only by landing its x there.  So each
+    // merge waits on the two sifts' LDS round trips alone.
+    uint16_t last = w.heap[U];                        // entry U - 1 after the build
+    // Merge step t pops from heaps of at most umax - t - 1 entries: the steps
+    // run in phases of one sift depth, floor(log2(umax - t - 1)) levels (the
+    // second pop's heap is one smaller: the same depth serves), so no step
+    // dispatches on its depth or loops to find it.
+    auto merge = [&](auto depth) {
+      constexpr int D = decltype(depth)::value;
       if (size > 1) {
         const uint16_t left = root;
         --size;
-        root = sift_levels<Cap>(w, l1, size, 0, w.heap[size + 1]);
+        const uint16_t e2 = w.heap[size];             // entry size - 1, before the sift
+        int fi;
+        root = sift_depth<Cap, D>(w, size, 0, last, &fi);
         const uint16_t right = root;
+        const uint16_t x2 = fi == size - 1 ? last : e2;
         --size;
-        root = sift_levels<Cap>(w, l2, size, 0, w.heap[size + 1]);
+        root = sift_depth<Cap, D>(w, size, 0, x2);
         const uint16_t merged = (uint16_t)((((left >> 8) + (right >> 8)) << 8) | next);
         w.heap[size + 1] = merged;                                              // not sifted up
+        last = merged;
         if constexpr (W::kTopDown) {
           // record of merged node m = next - U: left | right << 6 | leaves
           // under it << 12 | leaves under left << 17 (| DFS position << 22 |
@@ -299,7 +324,16 @@ __device__ bool tree_codes(const W &w, int U, uint32_t *__restrict__ table) {
         ++next;
         if (size == 1) root = merged;
       }
+    };
+    int t = 0;
+    if constexpr (Cap >= 17) {
+      for (; umax - t - 1 >= 16; ++t) merge(std::integral_constant<int, 4>{});
     }
+    if constexpr (Cap >= 9) {
+      for (; umax - t - 1 >= 8; ++t) merge(std::integral_constant<int, 3>{});
+    }
+    for (; umax - t - 1 >= 4; ++t) merge(std::integral_constant<int, 2>{});
+    for (; umax - t > 1; ++t) merge(std::integral_constant<int, 1>{});
   } else {
   for (int i = U / 2 - 1; i >= 0; --i) sift_any<Cap>(w, U, i, w.heap[i + 1]);
   root = w.heap[1];
@@ -678,10 +712,11 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
       // u & 1 of dword row u >> 1, so the store and the add share an address
       uint8_t *const sc = w.heap.p + ((lcw >> 1) << 8), *const sv = w.heap.p + ((lvw >> 1) << 8);
       const int hc = (lcw & 1) << 4, hv = (lvw & 1) << 4;
-      sc[hc >> 3] = (uint8_t)(kc - Off);
-      sv[hv >> 3] = (uint8_t)(kv - Off);
-      atomicAdd(reinterpret_cast<uint32_t *>(sc), (same ? 2u : 1u) << (hc + 8));
-      atomicAdd(reinterpret_cast<uint32_t *>(sv), (same ? 0u : 1u) << (hv + 8));
+      const bool fc = ec == 0, fv = !same && ev == 0;    // first occurrences
+      const uint32_t ac = (fc ? (uint32_t)(uint8_t)(kc - Off) : 0u) + ((same ? 2u : 1u) << 8);
+      const uint32_t av = (fv ? (uint32_t)(uint8_t)(kv - Off) : 0u) + ((same ? 0u : 1u) << 8);
+      atomicAdd(reinterpret_cast<uint32_t *>(sc), ac << hc);
+      atomicAdd(reinterpret_cast<uint32_t *>(sv), av << hv);
       U = min(nu2, Cap);
       lid[i / 3] |= (uint32_t)((lcw + 1) | ((lvw + 1) << 5)) << (10 * (i % 3));
     }
@@ -693,10 +728,13 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   }
   // (symbol | count << 8) per leaf -> the symbols (i8, 4 per dword) and the
   // heap entries (count << 8 | leaf at slot leaf + 1)
+  uint32_t h0[Cap];                                   // heap entry u: count << 8 | u
   {
     uint32_t sc[Cap / 2];
 #pragma unroll
     for (int k = 0; k < Cap / 2; ++k) sc[k] = *row(k);
+#pragma unroll
+    for (int u = 0; u < Cap; ++u) h0[u] = ((sc[u >> 1] >> (16 * (u & 1))) & 0xFF00u) | (uint32_t)u;
 #pragma unroll
     for (int j = 0; j < Cap / 4; ++j)
       *reinterpret_cast<uint32_t *>(w.sym.p + j * (4 * kLanes)) =
@@ -722,7 +760,7 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
     R += (lid[j] & 1023u ? 2 : 0) + ((lid[j] >> 10) & 1023u ? 2 : 0) + ((lid[j] >> 20) & 1023u ? 2 : 0);
 
   // ---- heap, tree and codes (JPEG.c:913-983): the table is dead ------------
-  bool over = tree_codes<Cap>(w, U, table + tile * kTablePerTile + bits_off(c));
+  bool over = tree_codes<Cap>(w, U, table + tile * kTablePerTile + bits_off(c), h0);
 
   // ---- encoded sequence, MSB-first (JPEG.c:993-1007) ------------------------
   uint32_t *const wout = reinterpret_cast<uint32_t *>(bits + tile * kBitsPerTile + bits_off(c));

@@ -1,0 +1,78 @@
+"""In-process A/B timing of entropy-encoder builds (tools only).
+
+    python3 tools/ab_ent_inproc.py [rounds] prod|<lib.so> ...
+
+A 4K random image's coefficients (the product DCT); every build (its own
+ctypes handle, RTLD_LOCAL) encodes them with jpegr_entropy_encode_device,
+round-robin after 100 ms of warm-up; per call torch events on the current
+stream.  Every build's bits / meta / table / status are compared with the
+first build's."""
+import ctypes
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "lz4-jpeg_amd")]
+import torch  # noqa: E402
+from lz4jpeg import jpeg, synth  # noqa: E402
+
+PROD = os.path.join(REPO, "lz4-jpeg_amd", "lz4jpeg", "liblz4jpeg.so")
+
+
+def main():
+    rounds = int(sys.argv[1])
+    names = sys.argv[2:]
+    libs = [ctypes.CDLL(PROD if a == "prod" else os.path.abspath(a), mode=ctypes.RTLD_LOCAL)
+            for a in names]
+    W, H = 3840, 2160
+    d_img = torch.from_numpy(synth.rand_rgba(W, H, seed=1)).cuda()
+    d_coef = jpeg.encode_device(d_img, W, H)
+    nt = jpeg.tiles(W, H)
+    libs[0].jpegr_entropy_scratch_bytes.restype = ctypes.c_size_t
+    sb = libs[0].jpegr_entropy_scratch_bytes(ctypes.c_size_t(nt))
+    outs = []
+    for _ in libs:
+        outs.append(dict(bits=torch.zeros(nt * 256, dtype=torch.uint8, device="cuda"),
+                         meta=torch.zeros(nt * 3, dtype=torch.int32, device="cuda"),
+                         table=torch.zeros(nt * 256, dtype=torch.int32, device="cuda"),
+                         status=torch.zeros(4, dtype=torch.int32, device="cuda"),
+                         scratch=torch.zeros(sb, dtype=torch.uint8, device="cuda")))
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = ctypes.c_void_p
+
+    def enc(k):
+        o = outs[k]
+        rc = libs[k].jpegr_entropy_encode_device(P(d_coef.data_ptr()), ctypes.c_size_t(nt),
+                                                 P(o["bits"].data_ptr()), P(o["meta"].data_ptr()),
+                                                 P(o["table"].data_ptr()), P(o["scratch"].data_ptr()),
+                                                 P(o["status"].data_ptr()), stream)
+        assert rc == 0, (names[k], rc)
+
+    for k in range(len(libs)):
+        enc(k)
+    torch.cuda.synchronize()
+    same = [all(torch.equal(outs[k][f], outs[0][f]) for f in ("bits", "meta", "table", "status"))
+            for k in range(len(libs))]
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.1:
+        for k in range(len(libs)):
+            enc(k)
+    torch.cuda.synchronize()
+    times = [[] for _ in libs]
+    for _ in range(rounds):
+        for k in range(len(libs)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            enc(k)
+            e1.record()
+            torch.cuda.synchronize()
+            times[k].append(e0.elapsed_time(e1))
+    for name, t, s in zip(names, times, same):
+        print(f"{os.path.basename(name):28s} encode median {statistics.median(t):.4f} min {min(t):.4f} ms"
+              f"  {'same' if s else 'DIFFERENT'}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
