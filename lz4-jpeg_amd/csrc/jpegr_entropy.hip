@@ -384,23 +384,21 @@ __device__ __forceinline__ bool tree_codes(const W &w, int U, uint32_t *__restri
     uint32_t pcode = 0;
     uint32_t de[Cap];
     int sy[Cap];
+    // (all Cap positions, no uniform branch per position: past a lane's U
+    // the entries are dead rows' values and nothing is stored)
 #pragma unroll
-    for (int k = 0; k < Cap; ++k)
-      if (k < umax) de[k] = w.dep[k];
+    for (int k = 0; k < Cap; ++k) de[k] = w.dep[k];
 #pragma unroll
-    for (int k = 0; k < Cap; ++k)
-      if (k < umax) sy[k] = w.sym[min((int)(de[k] >> 8), Cap - 1)];
+    for (int k = 0; k < Cap; ++k) sy[k] = w.sym[min((int)(de[k] >> 8), Cap - 1)];
 #pragma unroll
     for (int k = 0; k < Cap; ++k) {
-      if (k < umax) {
-        const int d = (int)(de[k] & 255u), x = min((int)(de[k] >> 8), Cap - 1);
-        const uint32_t t = k ? pcode + 1 : 0u;
-        pcode = d >= plen ? t << (d - plen) : t >> (plen - d);
-        plen = d;
-        if (k < U) {
-          w.code[x] = pcode | (uint32_t)d << 24;      // depth <= Cap - 1 < 24
-          table[k] = (uint16_t)sy[k] | ((uint32_t)d << 16);
-        }
+      const int d = (int)(de[k] & 255u), x = min((int)(de[k] >> 8), Cap - 1);
+      const uint32_t t = k ? pcode + 1 : 0u;
+      pcode = d >= plen ? t << (d - plen) : t >> (plen - d);
+      plen = d;
+      if (k < U) {
+        w.code[x] = pcode | (uint32_t)d << 24;        // depth <= Cap - 1 < 24
+        table[k] = (uint16_t)sy[k] | ((uint32_t)d << 16);
       }
     }
     return over;
