@@ -560,7 +560,13 @@ __device__ int encode_stream(const int16_t *__restrict__ zz, int n, const W &w,
 template <typename T>
 using GColT = Col<T>;
 
-// scratch header (in d_scratch): [0] deferred count, then the deferred list
+// Scratch (d_scratch): this header, then the chroma deferred list (2 ntiles
+// entries, the first ndefer used), the luma waves' deferred lists (64
+// entries per luma wave) and per luma wave a word deferred | overflowed << 8
+// (lanes), then the deferred pass's working set.  The luma kernel's wave 0
+// zeroes ndefer and status[0] before the chroma kernel runs; its own waves
+// report through their words, which entropy_encode_deferred reads, so no
+// init kernel precedes the encode.
 struct ScratchHdr {
   uint32_t ndefer;
   uint32_t pad[3];
@@ -643,7 +649,14 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   const int lane = threadIdx.x;
   const int c = kLuma ? 0 : 1 + (int)(blockIdx.x & 1);      // channel of this wave
   const size_t tile = (size_t)(kLuma ? blockIdx.x : blockIdx.x >> 1) * kLanes + lane;
+  if (kLuma && blockIdx.x == 0 && lane == 0) {       // for the chroma kernel and the caller
+    hdr->ndefer = 0;
+    status[0] = 0;
+  }
   if (tile >= ntiles) return;
+  // the luma waves' lists and words (see ScratchHdr)
+  uint32_t *const lst = deferred + 2 * ntiles + (size_t)blockIdx.x * kLanes;
+  uint32_t *const lword = deferred + 2 * ntiles + (size_t)gridDim.x * kLanes + blockIdx.x;
   auto colp = [&](uint32_t *row0) { return reinterpret_cast<uint8_t *>(row0 + lane); };
   uint8_t *const tabc = colp(&S.tab[0][0]);
   using HeapCol = typename std::conditional<L::Wide, WCol, LCol<uint16_t>>::type;
@@ -719,7 +732,17 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
       lid[i / 3] |= (uint32_t)((lcw + 1) | ((lvw + 1) << 5)) << (10 * (i % 3));
     }
   }
-  if (defer) {
+  uint64_t dm = 0;                                    // (luma) the wave's deferred lanes
+  if constexpr (kLuma) {
+    const uint64_t act = __ballot(1);
+    dm = __ballot(defer);
+    if (defer) lst[__popcll(dm & ((1ull << lane) - 1ull))] = (uint32_t)(tile * 3 + c);
+    if (dm == act) {                                  // (no lane left to report at the end)
+      if (lane == __builtin_ctzll(act)) *lword = (uint32_t)__popcll(dm);
+      return;
+    }
+    if (defer) return;
+  } else if (defer) {
     const uint32_t slot = atomicAdd(&hdr->ndefer, 1u);
     deferred[slot] = (uint32_t)(tile * 3 + c);
     return;
@@ -804,14 +827,20 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   if (nbits > ref_bits_max(c)) over = true;           // char sequence[1024] / [512]
   meta[tile * 3 + c] = (uint32_t)(nbits < 0xFFFF ? nbits : 0xFFFF) | ((uint32_t)R << 16) |
                        ((uint32_t)U << 24);
-  if (over) atomicAdd(&status[0], 1u);
+  if constexpr (kLuma) {
+    const uint64_t om = __ballot(over);
+    if (lane == __builtin_ctzll(__ballot(1)))
+      *lword = (uint32_t)__popcll(dm) | (uint32_t)__popcll(om) << 8;
+  } else if (over) {
+    atomicAdd(&status[0], 1u);
+  }
 }
 
 __global__ __launch_bounds__(kLanes) void entropy_encode_deferred(
     const int16_t *__restrict__ coef, uint8_t *__restrict__ bits, uint32_t *__restrict__ meta,
     uint32_t *__restrict__ table, const ScratchHdr *__restrict__ hdr,
-    const uint32_t *__restrict__ deferred, uint8_t *__restrict__ work,
-    uint32_t *__restrict__ status) {
+    const uint32_t *__restrict__ deferred, size_t ntiles, uint32_t luma_waves,
+    uint8_t *__restrict__ work, uint32_t *__restrict__ status) {
   const int gl = blockIdx.x * kLanes + threadIdx.x;          // this lane's scratch column
   constexpr int NL = kPass2Lanes;
   // column-per-lane arrays in global scratch (element i of lane gl at i*NL + gl)
@@ -823,9 +852,7 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_deferred(
   uint16_t *stk = reinterpret_cast<uint16_t *>(len + (size_t)NL * kFullCap);    // [Cap + 1]
   const Work<GColT> w{{sym + gl, NL}, {hash + gl, NL}, {heap + gl, NL},
                       {code + gl, NL}, {len + gl, NL}, {stk + gl, NL}};
-  const uint32_t nd = hdr->ndefer;
-  for (uint32_t i = gl; i < nd; i += NL) {
-    const uint32_t s = deferred[i];
+  auto encode = [&](uint32_t s) {
     const size_t tile = s / 3;
     const int c = (int)(s % 3);
     const int rc = encode_stream<kFullCap, 2 * kFullCap>(
@@ -833,7 +860,17 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_deferred(
         bits + tile * kBitsPerTile + bits_off(c), bits_cap(c), ref_bits_max(c),
         table + tile * kTablePerTile + bits_off(c), meta + tile * 3 + c);
     if (rc != kOk) atomicAdd(&status[0], 1u);
+  };
+  // the luma waves' words: their overflowed lanes and deferred lists
+  const uint32_t *const lst = deferred + 2 * ntiles;
+  const uint32_t *const lword = lst + (size_t)luma_waves * kLanes;
+  for (uint32_t v = gl; v < luma_waves; v += NL) {
+    const uint32_t x = lword[v];
+    if (x >> 8) atomicAdd(&status[0], x >> 8);
+    for (uint32_t j = 0; j < (x & 255u); ++j) encode(lst[(size_t)v * kLanes + j]);
   }
+  const uint32_t nd = hdr->ndefer;                    // the chroma kernel's list
+  for (uint32_t i = gl; i < nd; i += NL) encode(deferred[i]);
 }
 
 // bytes of the deferred pass's per-lane working set
@@ -1113,11 +1150,6 @@ __global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
   }
 }
 
-__global__ void entropy_init(ScratchHdr *hdr, uint32_t *status) {
-  hdr->ndefer = 0;
-  status[0] = 0;
-}
-
 // The decoder's luma and chroma kernels write disjoint outputs, and neither
 // fills the chip alone (a 4K image: 2,025 luma waves of 11.5 KB of LDS and
 // 2,025 chroma waves of 5.9 KB, each a single round of one-lane-per-stream
@@ -1160,8 +1192,14 @@ int run_side_by_side(hipStream_t s, F1 first, F2 second) {
 
 }  // namespace
 
+// the deferred lists and the luma waves' words (ScratchHdr)
+static size_t deferred_words(size_t ntiles) {
+  const size_t waves = (ntiles + kLanes - 1) / kLanes;
+  return 2 * ntiles + waves * (kLanes + 1);
+}
+
 extern "C" size_t jpegr_entropy_scratch_bytes(size_t ntiles) {
-  return 256 + ntiles * 3 * sizeof(uint32_t) + (size_t)kPass2Lanes * kWorkBytesPerLane;
+  return 256 + deferred_words(ntiles) * sizeof(uint32_t) + (size_t)kPass2Lanes * kWorkBytesPerLane;
 }
 
 extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, void *d_bits,
@@ -1174,9 +1212,8 @@ extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, vo
   hipStream_t s = static_cast<hipStream_t>(stream);
   auto *hdr = static_cast<ScratchHdr *>(d_scratch);
   auto *deferred = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_scratch) + 256);
-  auto *work = reinterpret_cast<uint8_t *>(deferred + ntiles * 3);
+  auto *work = reinterpret_cast<uint8_t *>(deferred + deferred_words(ntiles));
   auto *status = static_cast<uint32_t *>(d_status);
-  hipLaunchKernelGGL(entropy_init, dim3(1), dim3(1), 0, s, hdr, status);
   const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
   // (one stream: side by side, as the decoder runs, measured 0.140 -> 0.146 ms
   // per 4K image -- the encoder's luma and chroma waves contend for the same
@@ -1192,7 +1229,7 @@ extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, vo
   hipLaunchKernelGGL(entropy_encode_deferred, dim3(kPass2Lanes / kLanes), dim3(kLanes), 0, s,
                      static_cast<const int16_t *>(d_coef), static_cast<uint8_t *>(d_bits),
                      static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
-                     deferred, work, status);
+                     deferred, ntiles, groups, work, status);
   return hipGetLastError() == hipSuccess ? JPEGR_OK : JPEGR_ERR_HIP;
 }
 
