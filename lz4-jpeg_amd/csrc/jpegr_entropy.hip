@@ -47,7 +47,6 @@ constexpr int kLanes = 64;
 constexpr int kFastCap = 24;             // distinct symbols in the LDS pass (luma)
 constexpr int kChromaCap = 12;           // ... (chroma)
 constexpr int kFullCap = 128;            // RLE of 64 ints: <= 128 symbols
-constexpr int kPass2Lanes = 64 * 64;     // lanes of the deferred pass
 
 // per-tile output layout
 constexpr int kBitsPerTile = 256;        // bytes: [Y 128][Cr 64][Cb 64]
@@ -560,17 +559,10 @@ __device__ int encode_stream(const int16_t *__restrict__ zz, int n, const W &w,
 template <typename T>
 using GColT = Col<T>;
 
-// Scratch (d_scratch): this header, then the chroma deferred list (2 ntiles
-// entries, the first ndefer used), the luma waves' deferred lists (64
-// entries per luma wave) and per luma wave a word deferred | overflowed << 8
-// (lanes), then the deferred pass's working set.  The luma kernel's wave 0
-// zeroes ndefer and status[0] before the chroma kernel runs; its own waves
-// report through their words, which entropy_encode_deferred reads, so no
-// init kernel precedes the encode.
-struct ScratchHdr {
-  uint32_t ndefer;
-  uint32_t pad[3];
-};
+// Scratch (d_scratch): per luma wave a list of its deferred streams (64
+// entries), then per luma wave a word deferred | overflowed << 8 (lanes).
+// The chroma kernel reads them (its even wave 2 v: luma wave v), so no
+// kernel runs before the lane kernels or after them.
 
 // ---- the fast encoder: one lane per stream, no probing ------------------------
 // Symbols index a direct per-lane table (symbol + kOff -> leaf + 1, u8), so a
@@ -584,7 +576,8 @@ struct ScratchHdr {
 // registers (5 bits each, 3 positions per dword), so the sequence pass reads
 // only the codes.  The table is dead after the count: the DFS stack and the
 // codes overlay it.  A stream with a symbol outside the table or more than
-// Cap distinct symbols is deferred to entropy_encode_deferred.
+// Cap distinct symbols is deferred: the chroma kernel encodes it with the
+// hashed encoder after its own streams.
 template <int N>
 struct LaneLds {
   static constexpr int Cap = N == 64 ? kFastCap : kChromaCap;
@@ -640,8 +633,8 @@ struct LaneWork {                                     // the arrays tree_codes u
 template <bool kLuma>
 __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
     const int16_t *__restrict__ coef, size_t ntiles, uint8_t *__restrict__ bits,
-    uint32_t *__restrict__ meta, uint32_t *__restrict__ table, ScratchHdr *__restrict__ hdr,
-    uint32_t *__restrict__ deferred, uint32_t *__restrict__ status) {
+    uint32_t *__restrict__ meta, uint32_t *__restrict__ table, uint32_t *__restrict__ lists,
+    uint32_t *__restrict__ status) {
   constexpr int N = kLuma ? 64 : 32;
   using L = LaneLds<N>;
   constexpr int Cap = L::Cap, Keys = L::Keys, Off = L::Off;
@@ -649,14 +642,15 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   const int lane = threadIdx.x;
   const int c = kLuma ? 0 : 1 + (int)(blockIdx.x & 1);      // channel of this wave
   const size_t tile = (size_t)(kLuma ? blockIdx.x : blockIdx.x >> 1) * kLanes + lane;
-  if (kLuma && blockIdx.x == 0 && lane == 0) {       // for the chroma kernel and the caller
-    hdr->ndefer = 0;
-    status[0] = 0;
-  }
+  // (luma wave 0: the overflow count starts here; every later count is
+  // added by the chroma kernel)
+  if (kLuma && blockIdx.x == 0 && lane == 0) status[0] = 0;
   if (tile >= ntiles) return;
-  // the luma waves' lists and words (see ScratchHdr)
-  uint32_t *const lst = deferred + 2 * ntiles + (size_t)blockIdx.x * kLanes;
-  uint32_t *const lword = deferred + 2 * ntiles + (size_t)gridDim.x * kLanes + blockIdx.x;
+  // luma wave v's list and word (see the scratch layout above)
+  const size_t lv = kLuma ? blockIdx.x : blockIdx.x >> 1;
+  const size_t nlw = (ntiles + kLanes - 1) / kLanes;
+  uint32_t *const lst = lists + lv * kLanes;
+  uint32_t *const lword = lists + nlw * kLanes + lv;
   auto colp = [&](uint32_t *row0) { return reinterpret_cast<uint8_t *>(row0 + lane); };
   uint8_t *const tabc = colp(&S.tab[0][0]);
   using HeapCol = typename std::conditional<L::Wide, WCol, LCol<uint16_t>>::type;
@@ -742,142 +736,138 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
       return;
     }
     if (defer) return;
-  } else if (defer) {
-    const uint32_t slot = atomicAdd(&hdr->ndefer, 1u);
-    deferred[slot] = (uint32_t)(tile * 3 + c);
-    return;
+  } else {
+    dm = __ballot(defer);                             // encoded below, after the fast path
   }
-  // (symbol | count << 8) per leaf -> the symbols (i8, 4 per dword) and the
-  // heap entries (count << 8 | leaf at slot leaf + 1)
-  uint32_t h0[Cap];                                   // heap entry u: count << 8 | u
-  {
-    uint32_t sc[Cap / 2];
-#pragma unroll
-    for (int k = 0; k < Cap / 2; ++k) sc[k] = *row(k);
-#pragma unroll
-    for (int u = 0; u < Cap; ++u) h0[u] = ((sc[u >> 1] >> (16 * (u & 1))) & 0xFF00u) | (uint32_t)u;
-#pragma unroll
-    for (int j = 0; j < Cap / 4; ++j)
-      *reinterpret_cast<uint32_t *>(w.sym.p + j * (4 * kLanes)) =
-          __builtin_amdgcn_perm(sc[2 * j + 1], sc[2 * j], 0x06040200u);
-    if constexpr (L::Wide) {
-      // slot s (leaf s - 1) is row s
-#pragma unroll
-      for (int u = 0; u < Cap; ++u)
-        *row(u + 1) = ((sc[u >> 1] >> (16 * (u & 1))) & 0xFF00u) | (uint32_t)u;
-    } else {
-#pragma unroll
-      for (int r = 0; r < (Cap + 2) / 2; ++r) {
-        // slot 2r: leaf 2r - 1 (count: byte 3 of sc[r - 1]); slot 2r + 1: leaf 2r (byte 1 of sc[r])
-        const uint32_t lo = r > 0 ? (sc[r - 1] >> 16) & 0xFF00u : 0u;
-        const uint32_t hi = r < Cap / 2 ? (sc[r] & 0xFF00u) << 16 : 0u;
-        *row(r) = lo | hi | (uint32_t)(r > 0 ? 2 * r - 1 : 0) | (uint32_t)(2 * r) << 16;
+  if (!defer) {                                       // (luma: every lane left)
+    // (symbol | count << 8) per leaf -> the symbols (i8, 4 per dword) and the
+    // heap entries (count << 8 | leaf at slot leaf + 1)
+    uint32_t h0[Cap];                                   // heap entry u: count << 8 | u
+    {
+      uint32_t sc[Cap / 2];
+  #pragma unroll
+      for (int k = 0; k < Cap / 2; ++k) sc[k] = *row(k);
+  #pragma unroll
+      for (int u = 0; u < Cap; ++u) h0[u] = ((sc[u >> 1] >> (16 * (u & 1))) & 0xFF00u) | (uint32_t)u;
+  #pragma unroll
+      for (int j = 0; j < Cap / 4; ++j)
+        *reinterpret_cast<uint32_t *>(w.sym.p + j * (4 * kLanes)) =
+            __builtin_amdgcn_perm(sc[2 * j + 1], sc[2 * j], 0x06040200u);
+      if constexpr (L::Wide) {
+        // slot s (leaf s - 1) is row s
+  #pragma unroll
+        for (int u = 0; u < Cap; ++u)
+          *row(u + 1) = ((sc[u >> 1] >> (16 * (u & 1))) & 0xFF00u) | (uint32_t)u;
+      } else {
+  #pragma unroll
+        for (int r = 0; r < (Cap + 2) / 2; ++r) {
+          // slot 2r: leaf 2r - 1 (count: byte 3 of sc[r - 1]); slot 2r + 1: leaf 2r (byte 1 of sc[r])
+          const uint32_t lo = r > 0 ? (sc[r - 1] >> 16) & 0xFF00u : 0u;
+          const uint32_t hi = r < Cap / 2 ? (sc[r] & 0xFF00u) << 16 : 0u;
+          *row(r) = lo | hi | (uint32_t)(r > 0 ? 2 * r - 1 : 0) | (uint32_t)(2 * r) << 16;
+        }
+      }
+    }
+    int R = 0;
+  #pragma unroll
+    for (int j = 0; j < (N + 2) / 3; ++j)
+      R += (lid[j] & 1023u ? 2 : 0) + ((lid[j] >> 10) & 1023u ? 2 : 0) + ((lid[j] >> 20) & 1023u ? 2 : 0);
+
+    // ---- heap, tree and codes (JPEG.c:913-983): the table is dead ------------
+    bool over = tree_codes<Cap>(w, U, table + tile * kTablePerTile + bits_off(c), h0);
+
+    // ---- encoded sequence, MSB-first (JPEG.c:993-1007) ------------------------
+    uint32_t *const wout = reinterpret_cast<uint32_t *>(bits + tile * kBitsPerTile + bits_off(c));
+    constexpr int nwords = N / 2;                       // bits_cap / 32
+    // A leaf's code and length are one dword (code | length << 24); the reads
+    // do not depend on the bit accumulator, so each group of kG positions'
+    // code words is read while the previous group is shifted in.
+    const LCol<uint32_t> codez{colp(&S.tab[L::ZeroRow][0])};
+    codez[0] = 0u;
+    uint64_t acc = 0;
+    int nacc = 0, word = 0;
+    constexpr int kG = 4;
+    static_assert(N % kG == 0, "whole groups");
+    auto ident = [&](int i, int h) {                    // leaf + 1 of emission h at position i, 0: none
+      return (lid[i / 3] >> (10 * (i % 3) + 5 * h)) & 31u;
+    };
+    auto fetch = [&](int g, uint32_t (&cw)[2 * kG]) {
+  #pragma unroll
+      for (int j = 0; j < 2 * kG; ++j) {
+        cw[j] = codez[(int)ident(g * kG + j / 2, j & 1)];
+      }
+    };
+    uint32_t cur[2 * kG], nxt[2 * kG];
+    fetch(0, nxt);
+  #pragma unroll
+    for (int g = 0; g < N / kG; ++g) {
+  #pragma unroll
+      for (int j = 0; j < 2 * kG; ++j) cur[j] = nxt[j];
+      if (g + 1 < N / kG) fetch(g + 1, nxt);
+  #pragma unroll
+      for (int j = 0; j < 2 * kG; ++j) {
+        const int Lb = (int)(cur[j] >> 24);
+        acc = (acc << Lb) | (cur[j] & 0xFFFFFFu);
+        nacc += Lb;
+        const bool full = nacc >= 32;
+        nacc -= full ? 32 : 0;
+        if (full && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc >> nacc));
+        word += full ? 1 : 0;
+      }
+    }
+    const int nbits = 32 * word + nacc;
+    if (nacc && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc << (32 - nacc)));
+    if (nbits > ref_bits_max(c)) over = true;           // char sequence[1024] / [512]
+    meta[tile * 3 + c] = (uint32_t)(nbits < 0xFFFF ? nbits : 0xFFFF) | ((uint32_t)R << 16) |
+                         ((uint32_t)U << 24);
+    if constexpr (kLuma) {
+      const uint64_t om = __ballot(over);
+      if (lane == __builtin_ctzll(__ballot(1)))
+        *lword = (uint32_t)__popcll(dm) | (uint32_t)__popcll(om) << 8;
+    } else if (over) {
+      atomicAdd(&status[0], 1u);
+    }
+  }
+  if constexpr (!kLuma) {
+    // Deferred streams (a symbol outside the table or more than Cap
+    // distinct): the hashed encoder over this wave's LDS, which the fast path
+    // has left dead, one stream at a time on lane 0 -- the wave's own, then
+    // (an even wave) those of luma wave lv, whose overflowed lanes it counts.
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (lane == 0) {
+      const uint32_t lw = (blockIdx.x & 1) ? 0u : *lword;
+      if (lw >> 8) atomicAdd(&status[0], lw >> 8);
+      constexpr int kSymO = 0, kHashO = kSymO + 2 * kFullCap, kHeapO = kHashO + 2 * kFullCap;
+      constexpr int kCodeO = (kHeapO + 2 * (kFullCap + 2) + 3) & ~3, kLenO = kCodeO + 4 * kFullCap;
+      constexpr int kStkO = (kLenO + kFullCap + 1) & ~1, kEnd = kStkO + 2 * (kFullCap + 1);
+      static_assert(kEnd <= (int)sizeof(L), "the hashed encoder's arrays fit the wave's LDS");
+      uint8_t *const lb = reinterpret_cast<uint8_t *>(&S);
+      const Work<GColT> ws{{reinterpret_cast<int16_t *>(lb + kSymO), 1}, {lb + kHashO, 1},
+                           {reinterpret_cast<uint16_t *>(lb + kHeapO), 1},
+                           {reinterpret_cast<uint32_t *>(lb + kCodeO), 1}, {lb + kLenO, 1},
+                           {reinterpret_cast<uint16_t *>(lb + kStkO), 1}};
+      const int nown = __popcll(dm), n = nown + (int)(lw & 255u);
+      uint64_t own = dm;
+      for (int k = 0; k < n; ++k) {
+        uint32_t sid;                                 // tile * 3 + channel
+        if (k < nown) {
+          sid = (uint32_t)((lv * kLanes + __builtin_ctzll(own)) * 3 + c);
+          own &= own - 1;
+        } else {
+          sid = lst[k - nown];
+        }
+        const size_t t = sid / 3;
+        const int cc = (int)(sid % 3);
+        const int rc = encode_stream<kFullCap, 2 * kFullCap>(
+            coef + t * 128 + coef_off(cc), stream_len(cc), ws,
+            bits + t * kBitsPerTile + bits_off(cc), bits_cap(cc), ref_bits_max(cc),
+            table + t * kTablePerTile + bits_off(cc), meta + t * 3 + cc);
+        if (rc != kOk) atomicAdd(&status[0], 1u);
       }
     }
   }
-  int R = 0;
-#pragma unroll
-  for (int j = 0; j < (N + 2) / 3; ++j)
-    R += (lid[j] & 1023u ? 2 : 0) + ((lid[j] >> 10) & 1023u ? 2 : 0) + ((lid[j] >> 20) & 1023u ? 2 : 0);
-
-  // ---- heap, tree and codes (JPEG.c:913-983): the table is dead ------------
-  bool over = tree_codes<Cap>(w, U, table + tile * kTablePerTile + bits_off(c), h0);
-
-  // ---- encoded sequence, MSB-first (JPEG.c:993-1007) ------------------------
-  uint32_t *const wout = reinterpret_cast<uint32_t *>(bits + tile * kBitsPerTile + bits_off(c));
-  constexpr int nwords = N / 2;                       // bits_cap / 32
-  // A leaf's code and length are one dword (code | length << 24); the reads
-  // do not depend on the bit accumulator, so each group of kG positions'
-  // code words is read while the previous group is shifted in.
-  const LCol<uint32_t> codez{colp(&S.tab[L::ZeroRow][0])};
-  codez[0] = 0u;
-  uint64_t acc = 0;
-  int nacc = 0, word = 0;
-  constexpr int kG = 4;
-  static_assert(N % kG == 0, "whole groups");
-  auto ident = [&](int i, int h) {                    // leaf + 1 of emission h at position i, 0: none
-    return (lid[i / 3] >> (10 * (i % 3) + 5 * h)) & 31u;
-  };
-  auto fetch = [&](int g, uint32_t (&cw)[2 * kG]) {
-#pragma unroll
-    for (int j = 0; j < 2 * kG; ++j) {
-      cw[j] = codez[(int)ident(g * kG + j / 2, j & 1)];
-    }
-  };
-  uint32_t cur[2 * kG], nxt[2 * kG];
-  fetch(0, nxt);
-#pragma unroll
-  for (int g = 0; g < N / kG; ++g) {
-#pragma unroll
-    for (int j = 0; j < 2 * kG; ++j) cur[j] = nxt[j];
-    if (g + 1 < N / kG) fetch(g + 1, nxt);
-#pragma unroll
-    for (int j = 0; j < 2 * kG; ++j) {
-      const int Lb = (int)(cur[j] >> 24);
-      acc = (acc << Lb) | (cur[j] & 0xFFFFFFu);
-      nacc += Lb;
-      const bool full = nacc >= 32;
-      nacc -= full ? 32 : 0;
-      if (full && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc >> nacc));
-      word += full ? 1 : 0;
-    }
-  }
-  const int nbits = 32 * word + nacc;
-  if (nacc && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc << (32 - nacc)));
-  if (nbits > ref_bits_max(c)) over = true;           // char sequence[1024] / [512]
-  meta[tile * 3 + c] = (uint32_t)(nbits < 0xFFFF ? nbits : 0xFFFF) | ((uint32_t)R << 16) |
-                       ((uint32_t)U << 24);
-  if constexpr (kLuma) {
-    const uint64_t om = __ballot(over);
-    if (lane == __builtin_ctzll(__ballot(1)))
-      *lword = (uint32_t)__popcll(dm) | (uint32_t)__popcll(om) << 8;
-  } else if (over) {
-    atomicAdd(&status[0], 1u);
-  }
 }
-
-__global__ __launch_bounds__(kLanes) void entropy_encode_deferred(
-    const int16_t *__restrict__ coef, uint8_t *__restrict__ bits, uint32_t *__restrict__ meta,
-    uint32_t *__restrict__ table, const ScratchHdr *__restrict__ hdr,
-    const uint32_t *__restrict__ deferred, size_t ntiles, uint32_t luma_waves,
-    uint8_t *__restrict__ work, uint32_t *__restrict__ status) {
-  const int gl = blockIdx.x * kLanes + threadIdx.x;          // this lane's scratch column
-  constexpr int NL = kPass2Lanes;
-  // column-per-lane arrays in global scratch (element i of lane gl at i*NL + gl)
-  int16_t *sym = reinterpret_cast<int16_t *>(work);                             // [Cap]
-  uint8_t *hash = work + (size_t)NL * 2 * kFullCap;                             // [2 Cap]
-  uint16_t *heap = reinterpret_cast<uint16_t *>(hash + (size_t)NL * 2 * kFullCap);   // [Cap]
-  uint32_t *code = reinterpret_cast<uint32_t *>(heap + (size_t)NL * (kFullCap + 2));  // [Cap]
-  uint8_t *len = reinterpret_cast<uint8_t *>(code + (size_t)NL * kFullCap);     // [Cap]
-  uint16_t *stk = reinterpret_cast<uint16_t *>(len + (size_t)NL * kFullCap);    // [Cap + 1]
-  const Work<GColT> w{{sym + gl, NL}, {hash + gl, NL}, {heap + gl, NL},
-                      {code + gl, NL}, {len + gl, NL}, {stk + gl, NL}};
-  auto encode = [&](uint32_t s) {
-    const size_t tile = s / 3;
-    const int c = (int)(s % 3);
-    const int rc = encode_stream<kFullCap, 2 * kFullCap>(
-        coef + tile * 128 + coef_off(c), stream_len(c), w,
-        bits + tile * kBitsPerTile + bits_off(c), bits_cap(c), ref_bits_max(c),
-        table + tile * kTablePerTile + bits_off(c), meta + tile * 3 + c);
-    if (rc != kOk) atomicAdd(&status[0], 1u);
-  };
-  // the luma waves' words: their overflowed lanes and deferred lists
-  const uint32_t *const lst = deferred + 2 * ntiles;
-  const uint32_t *const lword = lst + (size_t)luma_waves * kLanes;
-  for (uint32_t v = gl; v < luma_waves; v += NL) {
-    const uint32_t x = lword[v];
-    if (x >> 8) atomicAdd(&status[0], x >> 8);
-    for (uint32_t j = 0; j < (x & 255u); ++j) encode(lst[(size_t)v * kLanes + j]);
-  }
-  const uint32_t nd = hdr->ndefer;                    // the chroma kernel's list
-  for (uint32_t i = gl; i < nd; i += NL) encode(deferred[i]);
-}
-
-// bytes of the deferred pass's per-lane working set
-constexpr size_t kWorkBytesPerLane = 2 * kFullCap /*sym*/ + 2 * kFullCap /*hash*/ +
-                                     2 * (kFullCap + 2) /*heap + children*/ +
-                                     4 * kFullCap /*code*/ + kFullCap /*len*/ +
-                                     2 * (kFullCap + 1) /*stk*/;
 
 // ---- decode ------------------------------------------------------------------
 
@@ -1192,14 +1182,9 @@ int run_side_by_side(hipStream_t s, F1 first, F2 second) {
 
 }  // namespace
 
-// the deferred lists and the luma waves' words (ScratchHdr)
-static size_t deferred_words(size_t ntiles) {
-  const size_t waves = (ntiles + kLanes - 1) / kLanes;
-  return 2 * ntiles + waves * (kLanes + 1);
-}
-
+// the luma waves' deferred lists and words (the scratch layout above)
 extern "C" size_t jpegr_entropy_scratch_bytes(size_t ntiles) {
-  return 256 + deferred_words(ntiles) * sizeof(uint32_t) + (size_t)kPass2Lanes * kWorkBytesPerLane;
+  return (ntiles + kLanes - 1) / kLanes * (kLanes + 1) * sizeof(uint32_t);
 }
 
 extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, void *d_bits,
@@ -1210,9 +1195,7 @@ extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, vo
       (reinterpret_cast<uintptr_t>(d_bits) & 3) != 0)
     return JPEGR_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  auto *hdr = static_cast<ScratchHdr *>(d_scratch);
-  auto *deferred = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_scratch) + 256);
-  auto *work = reinterpret_cast<uint8_t *>(deferred + deferred_words(ntiles));
+  auto *lists = static_cast<uint32_t *>(d_scratch);
   auto *status = static_cast<uint32_t *>(d_status);
   const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
   // (one stream: side by side, as the decoder runs, measured 0.140 -> 0.146 ms
@@ -1220,16 +1203,12 @@ extern "C" int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, vo
   // LDS and issue slots, and the fork / join costs more than it overlaps)
   hipLaunchKernelGGL(entropy_encode_lane<true>, dim3(groups), dim3(kLanes), 0, s,
                      static_cast<const int16_t *>(d_coef), ntiles, static_cast<uint8_t *>(d_bits),
-                     static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
-                     deferred, status);
+                     static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), lists,
+                     status);
   hipLaunchKernelGGL(entropy_encode_lane<false>, dim3(groups * 2), dim3(kLanes), 0, s,
                      static_cast<const int16_t *>(d_coef), ntiles, static_cast<uint8_t *>(d_bits),
-                     static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
-                     deferred, status);
-  hipLaunchKernelGGL(entropy_encode_deferred, dim3(kPass2Lanes / kLanes), dim3(kLanes), 0, s,
-                     static_cast<const int16_t *>(d_coef), static_cast<uint8_t *>(d_bits),
-                     static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), hdr,
-                     deferred, ntiles, groups, work, status);
+                     static_cast<uint32_t *>(d_meta), static_cast<uint32_t *>(d_table), lists,
+                     status);
   return hipGetLastError() == hipSuccess ? JPEGR_OK : JPEGR_ERR_HIP;
 }
 
