@@ -684,7 +684,7 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   uint32_t lid[(N + 2) / 3];             // per position: (leaf_c + 1) | (leaf_v + 1) << 5
 #pragma unroll
   for (int j = 0; j < (N + 2) / 3; ++j) lid[j] = 0;
-  int U = 0, start = 0;
+  int U = 0, start = 0, R = 0;
   bool defer = false;
   // One exec region per position and no branch inside it: the stores are
   // unconditional and idempotent (a known symbol rewrites its table entry and
@@ -723,6 +723,7 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
       atomicAdd(reinterpret_cast<uint32_t *>(sc), ac << hc);
       atomicAdd(reinterpret_cast<uint32_t *>(sv), av << hv);
       U = min(nu2, Cap);
+      R += 2;                                         // the run's (count, value)
       lid[i / 3] |= (uint32_t)((lcw + 1) | ((lvw + 1) << 5)) << (10 * (i % 3));
     }
   }
@@ -745,21 +746,21 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
     uint32_t h0[Cap];                                   // heap entry u: count << 8 | u
     {
       uint32_t sc[Cap / 2];
-  #pragma unroll
+#pragma unroll
       for (int k = 0; k < Cap / 2; ++k) sc[k] = *row(k);
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < Cap; ++u) h0[u] = ((sc[u >> 1] >> (16 * (u & 1))) & 0xFF00u) | (uint32_t)u;
-  #pragma unroll
+#pragma unroll
       for (int j = 0; j < Cap / 4; ++j)
         *reinterpret_cast<uint32_t *>(w.sym.p + j * (4 * kLanes)) =
             __builtin_amdgcn_perm(sc[2 * j + 1], sc[2 * j], 0x06040200u);
       if constexpr (L::Wide) {
         // slot s (leaf s - 1) is row s
-  #pragma unroll
+#pragma unroll
         for (int u = 0; u < Cap; ++u)
           *row(u + 1) = ((sc[u >> 1] >> (16 * (u & 1))) & 0xFF00u) | (uint32_t)u;
       } else {
-  #pragma unroll
+#pragma unroll
         for (int r = 0; r < (Cap + 2) / 2; ++r) {
           // slot 2r: leaf 2r - 1 (count: byte 3 of sc[r - 1]); slot 2r + 1: leaf 2r (byte 1 of sc[r])
           const uint32_t lo = r > 0 ? (sc[r - 1] >> 16) & 0xFF00u : 0u;
@@ -768,10 +769,6 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
         }
       }
     }
-    int R = 0;
-  #pragma unroll
-    for (int j = 0; j < (N + 2) / 3; ++j)
-      R += (lid[j] & 1023u ? 2 : 0) + ((lid[j] >> 10) & 1023u ? 2 : 0) + ((lid[j] >> 20) & 1023u ? 2 : 0);
 
     // ---- heap, tree and codes (JPEG.c:913-983): the table is dead ------------
     bool over = tree_codes<Cap>(w, U, table + tile * kTablePerTile + bits_off(c), h0);
@@ -792,19 +789,19 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
       return (lid[i / 3] >> (10 * (i % 3) + 5 * h)) & 31u;
     };
     auto fetch = [&](int g, uint32_t (&cw)[2 * kG]) {
-  #pragma unroll
+#pragma unroll
       for (int j = 0; j < 2 * kG; ++j) {
         cw[j] = codez[(int)ident(g * kG + j / 2, j & 1)];
       }
     };
     uint32_t cur[2 * kG], nxt[2 * kG];
     fetch(0, nxt);
-  #pragma unroll
+#pragma unroll
     for (int g = 0; g < N / kG; ++g) {
-  #pragma unroll
+#pragma unroll
       for (int j = 0; j < 2 * kG; ++j) cur[j] = nxt[j];
       if (g + 1 < N / kG) fetch(g + 1, nxt);
-  #pragma unroll
+#pragma unroll
       for (int j = 0; j < 2 * kG; ++j) {
         const int Lb = (int)(cur[j] >> 24);
         acc = (acc << Lb) | (cur[j] & 0xFFFFFFu);
