@@ -792,7 +792,7 @@ def run_jpeg(ctx, total_images, scaling):
         "value": round(px / (enc_ms / 1e3) / 1e9, 3), "unit": "Gpixel/s", "images": 1,
         "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4), "warmup": ewarm,
         "decode_gpix_s": round(px / (dec_ms / 1e3) / 1e9, 3),
-        "kernels": ["entropy_encode_lane", "entropy_encode_deferred", "entropy_decode_kernel"],
+        "kernels": ["entropy_encode_lane", "entropy_decode_kernel"],
         "bits_per_pixel": round(sum_bits / px, 4), "roundtrip_ok": ent_ok,
         "roofline": {"bound": "issue (serial per-stream integer work)", "unit": "GB/s",
                      "hbm_achieved": round(ebytes / (enc_ms / 1e3) / 1e9, 2),

@@ -30,9 +30,10 @@
 // sequence -- one stream per wave step, ballots and LDS atomics -- measured
 // 0.34 ms: 64 dependent steps per wave, same-address atomics serialised.)
 // Streams with a symbol outside the table or more than 24 (luma) / 12
-// (chroma) distinct symbols (random 4K tiles: Y <= 21, chroma <= 10) go to a
-// second pass running the hashed encoder over global-memory scratch with
-// room for 128.
+// (chroma) distinct symbols (random 4K tiles: Y <= 21, chroma <= 10) are
+// encoded by the chroma kernel after its own streams, with the hashed
+// encoder (room for 128) over the wave's LDS.  Two kernels per call: luma,
+// then chroma.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
