@@ -348,6 +348,13 @@ def run_lz4(ctx, n_total, scaling):
         ctx.host_text = synth.random_passages(min(n, 1 << 30), length=30000, seed=1, first=lo)
     d_in = torch.empty(n + 16, dtype=torch.uint8, device=dev)
     synth.random_passages_device(d_in, n, length=30000, seed=1, first=lo)
+    # clock pre-warm, not a warm-up step: ~100 ms of unrelated device work
+    # (elementwise passes over 256 MB) so that the W warm-up steps already run
+    # at the held clock and a kernel trace's average over every launch of the
+    # run agrees with the timed steps (settle())
+    d_warm = torch.zeros(256 << 20, dtype=torch.uint8, device=dev)
+    settle(lambda: d_warm.add_(1), torch.cuda.synchronize, ms=100.0, chunk=16)
+    del d_warm
     comp = lz4.Compressor()
     # text grows by ~3.5 %; the call reports the need if a shard ever exceeds this
     cap = n + n // 8 + (1 << 20)

@@ -1,12 +1,13 @@
-"""In-process A/B timing of entropy-encoder builds (tools only).
+"""In-process A/B timing of entropy-stage builds (tools only).
 
     python3 tools/ab_ent_inproc.py [rounds] prod|<lib.so> ...
 
 A 4K random image's coefficients (the product DCT); every build (its own
 ctypes handle, RTLD_LOCAL) encodes them with jpegr_entropy_encode_device,
 round-robin after 100 ms of warm-up; per call torch events on the current
-stream.  Every build's bits / meta / table / status are compared with the
-first build's."""
+stream; then each build decodes its own encoding (jpegr_entropy_decode_device,
+timed the same way).  Every build's bits / meta / table / status are compared
+with the first build's, and every decode with the coefficients."""
 import ctypes
 import os
 import statistics
@@ -38,7 +39,8 @@ def main():
                          meta=torch.zeros(nt * 3, dtype=torch.int32, device="cuda"),
                          table=torch.zeros(nt * 256, dtype=torch.int32, device="cuda"),
                          status=torch.zeros(4, dtype=torch.int32, device="cuda"),
-                         scratch=torch.zeros(sb, dtype=torch.uint8, device="cuda")))
+                         scratch=torch.zeros(sb, dtype=torch.uint8, device="cuda"),
+                         back=torch.zeros_like(d_coef)))
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     P = ctypes.c_void_p
 
@@ -50,6 +52,21 @@ def main():
                                                  P(o["status"].data_ptr()), stream)
         assert rc == 0, (names[k], rc)
 
+    def dec(k):
+        o = outs[k]
+        rc = libs[k].jpegr_entropy_decode_device(P(o["bits"].data_ptr()), P(o["meta"].data_ptr()),
+                                                 P(o["table"].data_ptr()), ctypes.c_size_t(nt),
+                                                 P(o["back"].data_ptr()), P(o["status"].data_ptr()),
+                                                 stream)
+        assert rc == 0, (names[k], rc)
+
+    for k in range(len(libs)):
+        enc(k)
+    torch.cuda.synchronize()
+    for k in range(len(libs)):
+        dec(k)
+    torch.cuda.synchronize()
+    back_ok = [bool(torch.equal(o["back"], d_coef)) for o in outs]
     for k in range(len(libs)):
         enc(k)
     torch.cuda.synchronize()
@@ -61,17 +78,22 @@ def main():
             enc(k)
     torch.cuda.synchronize()
     times = [[] for _ in libs]
+    dtimes = [[] for _ in libs]
     for _ in range(rounds):
         for k in range(len(libs)):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
             e0.record()
             enc(k)
             e1.record()
+            dec(k)
+            e2.record()
             torch.cuda.synchronize()
             times[k].append(e0.elapsed_time(e1))
-    for name, t, s in zip(names, times, same):
+            dtimes[k].append(e1.elapsed_time(e2))
+    for name, t, d, s, b in zip(names, times, dtimes, same, back_ok):
         print(f"{os.path.basename(name):28s} encode median {statistics.median(t):.4f} min {min(t):.4f} ms"
-              f"  {'same' if s else 'DIFFERENT'}", flush=True)
+              f"  {'same' if s else 'DIFFERENT'}  decode median {statistics.median(d):.4f}"
+              f" min {min(d):.4f} ms  {'ok' if b else 'DECODE MISMATCH'}", flush=True)
 
 
 if __name__ == "__main__":
