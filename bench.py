@@ -22,6 +22,8 @@ seeded generators; a step is one pass of the hot path over the rank's share
 with inputs resident in HBM.  Rank 0 prints one JSON line.
 """
 import argparse
+import datetime
+import faulthandler
 import json
 import os
 import socket
@@ -120,8 +122,8 @@ def issue_roof(bytes_now, launch_ms):
     LDS-array cycles, all from one profiled run on one box (counts, time and
     clock of the same dispatches).  frac = the largest pipe's CU cycles per
     block / the measured CU cycles per block of that run (<= 1: lower
-    bounds); frac_live prices this bench's own lz4_tiles time at the
-    profile's clock."""
+    bounds) of this bench's own lz4_tiles time priced at the profile's
+    clock; profile_frac is the profiled run's fraction."""
     try:
         d = json.load(open(_profile_json(ROOF_JSON)))
         roof = d["roof_cu_cycles_per_block"]
@@ -136,9 +138,11 @@ def issue_roof(bytes_now, launch_ms):
         "roof_cu_cycles_per_block": roof, "binding_pipe": bind,
         "measured_cu_cycles_per_block": meas["cu_cycles_per_block"],
         "profile_clock_ghz": meas["clock_ghz"], "profile_ms": meas["ms"],
-        "frac": d["frac"], "frac_by_pipe": d["frac_by_pipe"],
+        # frac: this run's lz4_tiles time priced at the profile's clock;
+        # profile_frac: the profiled run's own fraction (static, from the file)
+        "frac": round(roof[bind] / live_cyc, 4),
+        "profile_frac": d["frac"], "profile_frac_by_pipe": d["frac_by_pipe"],
         "live_cu_cycles_per_block_at_profile_clock": round(live_cyc, 1),
-        "frac_live": round(roof[bind] / live_cyc, 4),
         "per_block": d["per_block"],
         "note": "from " + os.path.basename(_profile_json(ROOF_JSON)) + " (tools/roof.py): "
                 "VALU = lower bound of the vector-issue cycles per block per SIMD "
@@ -187,6 +191,16 @@ def maybe_self_launch(args, argv, env=None):
     child_env = dict(env)
     child_env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=child_env)
+
+
+def phase(name, rank, limit_s):
+    """Mark the start of a bench phase on this rank.  If the phase has not
+    ended `limit_s` seconds later (a collective that never completes, a
+    stuck kernel), every thread's stack is dumped to stderr and the rank
+    exits non-zero, so a first-time 8-GPU run fails with the phase named
+    instead of being killed silently at the driver's limit."""
+    log(f"rank {rank}: phase {name}")
+    faulthandler.dump_traceback_later(limit_s, exit=True)
 
 
 def rank_env(env=None):
@@ -252,6 +266,9 @@ def main(argv=None):
                     help="run the N > 1 code path (RCCL process group, sharded config-4/5 "
                          "workloads, length all_gather, gatherv) even at one rank: the "
                          "world-size-1 rehearsal of the 8-GPU job")
+    ap.add_argument("--dist-timeout", type=float, default=120.0,
+                    help="seconds: the process group's collective timeout (RCCL watchdog "
+                         "aborts the rank) and the per-phase watchdog of every rank")
     ap.add_argument("--launch-check", action="store_true",
                     help="print each rank's (rank, world, local rank, shares) and exit "
                          "without touching the GPU (tests the launcher plumbing)")
@@ -280,12 +297,19 @@ def main(argv=None):
     dev = torch.device("cuda", local)
     multi = world > 1 or args.dist       # the distributed code path
     if multi:
-        dist.init_process_group("nccl", device_id=dev)
+        # a collective that has not completed after dist_timeout aborts the
+        # rank (the RCCL watchdog tears the communicator down, the process
+        # exits non-zero) -- well inside the driver's 600 s for the run
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "3")
+        phase("init_process_group", rank, args.dist_timeout + 60)
+        dist.init_process_group("nccl", device_id=dev,
+                                timeout=datetime.timedelta(seconds=args.dist_timeout))
     ctx = Ctx(world, rank, dev, args, torch, dist, multi)
     lz4_total, jpeg_total, scaling = workloads(world, args)
 
     line = run_lz4(ctx, lz4_total, scaling)
     if not args.no_jpeg:
+        ctx.phase("jpeg")
         line["jpeg"] = run_jpeg(ctx, jpeg_total, scaling)
     else:
         line["jpeg"] = None
@@ -298,7 +322,9 @@ def main(argv=None):
     if rank == 0:
         print(json.dumps(line), flush=True)
     if multi:
+        phase("destroy_process_group", rank, args.dist_timeout + 60)
         dist.destroy_process_group()
+    faulthandler.cancel_dump_traceback_later()
 
 
 class Ctx:
@@ -311,9 +337,22 @@ class Ctx:
         self.host_text = None
         self.host_img = None
 
+    def phase(self, name):
+        if self.multi:
+            phase(name, self.rank, self.args.dist_timeout + 60)
+
     def barrier(self):
         if self.multi:
             self.dist.barrier()
+
+    def all_ranks(self, x):
+        """[x of rank 0, ..., x of rank W-1] (a float per rank)."""
+        if not self.multi:
+            return [x]
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        g = self.torch.empty(self.world, dtype=self.torch.float64, device=self.dev)
+        self.dist.all_gather_into_tensor(g, t)
+        return [float(v) for v in g.cpu().tolist()]
 
     def max_over_ranks(self, x):
         if not self.multi:
@@ -360,63 +399,100 @@ def run_lz4(ctx, n_total, scaling):
     cap = n + n // 8 + (1 << 20)
     d_out = torch.empty(1 + cap, dtype=torch.uint8, device=dev)   # [frame byte] + segment
     d_len = torch.zeros(1, dtype=torch.int64, device=dev)
+    # N = 1: one int64 length slot per call (warm-up and timed), so every
+    # call's length -- and its corrupt-index bit 63 -- survives to be checked
+    # after the timed region
+    d_lens = torch.zeros(max(1, args.warmup + args.steps), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
 
-    def lz4_step():
+    def lz4_step(i):
         if not ctx.multi:
             # stream-ordered, as a device-resident pipeline runs it: the length
-            # stays in HBM (d_len) and is read once after the timed steps, so
-            # consecutive calls queue back to back with no host round trip
-            comp.compress_async(d_in, n, d_out, d_len)
+            # stays in HBM (slot i of d_lens) and is read after the timed steps,
+            # so consecutive calls queue back to back with no host round trip
+            comp.compress_async(d_in, n, d_out, d_lens[i:i + 1])
             return None
         comp.compress_async(d_in, n, d_out[1:], d_len, segment=True, final_shard=final_shard)
         # the raw signed length (negative: a corrupt LDS index); exchange_lengths
         # gathers it first and then raises on every rank (raising here would
-        # leave the other ranks waiting in the collective)
+        # leave the other ranks waiting in the collective).  This read-back +
+        # all_gather is part of the N > 1 step: the gather offsets need it
         seg = int(d_len.item())
         ldist.exchange_lengths(seg, dev)
         return seg
 
-    def step_length(got):
-        return comp.async_length(d_len) if got is None else got
+    def slot_lengths(i0, i1):
+        """Lengths of the N = 1 calls i0..i1-1 (one read-back); raises on a
+        corrupt verdict in any of them."""
+        vals = [int(v) for v in d_lens[i0:i1].cpu().tolist()]
+        bad = [i0 + k for k, v in enumerate(vals) if v < 0]
+        if bad:
+            raise lz4.Lz4Error(-6, f"lz4: calls {bad} flagged a corrupt LDS index")
+        return vals
 
     # the per-call timing events are created and first recorded in the warm-up
     # steps (their one-off cost would otherwise land in the timed steps)
+    ctx.phase("lz4 warm-up")
     comp.set_timing(True)
-    for _ in range(args.warmup):
-        out_len = lz4_step()
-    out_len = step_length(out_len) if args.warmup else None
+    out_len = None
+    for i in range(args.warmup):
+        out_len = lz4_step(i)
+    if args.warmup and not ctx.multi:
+        warm = slot_lengths(0, args.warmup)
+        if len(set(warm)) != 1:
+            raise RuntimeError(f"lz4: warm-up call lengths differ: {sorted(set(warm))}")
+        out_len = warm[-1]
     if out_len is not None and out_len > cap:
         raise RuntimeError(f"lz4: output {out_len} B exceeds the bench buffer {cap} B")
     torch.cuda.synchronize()
     ctx.barrier()
     comp.set_timing(True)                  # a new record: the timed calls only
     torch.cuda.synchronize()
+    ctx.phase("lz4 timed steps")
     ctx.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        got = lz4_step()
+    for i in range(args.steps):
+        got = lz4_step(args.warmup + i)
     torch.cuda.synchronize()
+    t_rank = time.perf_counter() - t0      # this rank's own time, before the barrier
     ctx.barrier()
     dt = ctx.max_over_ranks(time.perf_counter() - t0)
-    timed_len = step_length(got)
-    if out_len is not None and timed_len != out_len:
-        raise RuntimeError(f"lz4: timed call length {timed_len} != warm-up length {out_len}")
-    out_len = timed_len
+    if not ctx.multi:
+        lens_timed = slot_lengths(args.warmup, args.warmup + args.steps)
+        if out_len is not None and any(v != out_len for v in lens_timed):
+            raise RuntimeError(f"lz4: timed call lengths {sorted(set(lens_timed))} != "
+                               f"warm-up length {out_len}")
+        out_len = lens_timed[-1]
+    else:
+        out_len = got
     call_ms, match_ms = comp.timed_calls(args.steps)
     comp.set_timing(False)
     lz4_ms = dt / args.steps * 1e3
     lz4_gbs = n_total / (dt / args.steps) / 1e9
-    avg_match_ms = ctx.max_over_ranks(sum(match_ms) / len(match_ms))
-    avg_call_ms = ctx.max_over_ranks(sum(call_ms) / len(call_ms))
+    rank_match_ms = ctx.all_ranks(sum(match_ms) / len(match_ms))
+    rank_call_ms = ctx.all_ranks(sum(call_ms) / len(call_ms))
+    rank_step_ms = ctx.all_ranks(t_rank / args.steps * 1e3)
+    avg_match_ms = max(rank_match_ms)
+    avg_call_ms = max(rank_call_ms)
     out_total = ctx.sum_over_ranks(out_len) + (1 if ctx.multi else 0)
     cs = sorted(call_ms)
     log(f"lz4: {lz4_ms:.3f} ms/step, {lz4_gbs:.1f} GB/s aggregate, lz4_tiles "
         f"{avg_match_ms:.3f} ms, call {avg_call_ms:.3f} ms, out {out_total} B; call "
         f"min/median/max {cs[0]:.3f}/{cs[len(cs) // 2]:.3f}/{cs[-1]:.3f} ms")
+    per_rank = None
+    if ctx.multi:
+        per_rank = {
+            "call_ms": [round(v, 4) for v in rank_call_ms],
+            "lz4_tiles_ms": [round(v, 4) for v in rank_match_ms],
+            "step_ms": [round(v, 4) for v in rank_step_ms],
+            "call_ms_min_max": [round(min(rank_call_ms), 4), round(max(rank_call_ms), 4)],
+            "note": "per rank: average compress call and lz4_tiles time (library HIP events) "
+                    "and the rank's own step time before the closing barrier"}
+        log(f"lz4 per rank: call ms {per_rank['call_ms']}, step ms {per_rank['step_ms']}")
 
     # decoder (SURVEY 8f row 1): this rank's blocks -> bytes, in HBM, with the
     # compressor's device-resident block offsets (no host round trip)
+    ctx.phase("lz4 decode")
     nb_local = ldist.nblocks(n)
     if not ctx.multi:
         _, flen = comp.compress_device(d_in, n, d_out)
@@ -459,6 +535,7 @@ def run_lz4(ctx, n_total, scaling):
     }
     log(f"lz4 decode: {dec_kern_ms:.3f} ms/launch, {lz4_dec['value']} GB/s, ok={dec_ok}")
 
+    ctx.phase("lz4 bare-stream decode")
     # the same stream decoded from the bytes alone (LZ4_decode, LZ4.c:1038):
     # block boundaries found on the device, then the block decoder
     d_dec = torch.empty(n + 300, dtype=torch.uint8, device=dev)
@@ -489,6 +566,7 @@ def run_lz4(ctx, n_total, scaling):
     # N > 1: assemble the framed stream on rank 0 (RCCL gatherv over xGMI)
     gather_ms = gather_ok = None
     if ctx.multi:
+        ctx.phase("lz4 gather")
         comp.compress_async(d_in, n, d_out[1:], d_len, segment=True, final_shard=final_shard)
         seg = int(d_len.item())              # raw: exchange_lengths raises on every rank
         lens, offs = ldist.exchange_lengths(seg, dev)
@@ -504,7 +582,8 @@ def run_lz4(ctx, n_total, scaling):
             gather_ok = (int(full[0].item()) == ldist.nblocks(n_total) & 0xFF and
                          bool(torch.equal(full[1:1 + seg], d_out[1:1 + seg])))
             del full
-        log(f"lz4 gather: {gather_ms:.2f} ms for {sum(lens) + 1} B")
+        log(f"lz4 gather: {gather_ms:.2f} ms for {sum(lens) + 1} B in pieces of "
+            f"<= {ldist.GATHER_CHUNK} B")
 
     # N = 1: one GPU's share of config 4 (the 8-GPU job's rank-0 shard: the
     # first 8 GiB of the 64 GiB corpus) with the N > 1 step -- a segment
@@ -551,12 +630,16 @@ def run_lz4(ctx, n_total, scaling):
                 "newlines->spaces, glibc rand seed 1; each rank synthesises its shard in HBM",
         "config": {"workload": cfg, "bytes_per_rank": n, "bytes_total": n_total, "block": 300,
                    "parallelism": f"shard{world}", "compressed_bytes_total": out_total,
-                   "step": ("compress" if not ctx.multi else
-                            "segment compress + all_gather of segment lengths")},
+                   "step": ("compress (stream-ordered: the K calls queue back to back, each "
+                            "call's length read after the timed region)" if not ctx.multi else
+                            "segment compress + length read-back + all_gather of segment "
+                            "lengths (a host round trip per step)")},
         "roofline": roof_lz4,
         "cpu_baseline": None,
         "lz4_gather_ms": None if gather_ms is None else round(gather_ms, 3),
         "lz4_gather_ok": gather_ok,
+        "lz4_gather_chunk_bytes": ldist.GATHER_CHUNK if ctx.multi else None,
+        "per_rank": per_rank,
         "value_incl_gather": (None if gather_ms is None else
                               round(n_total / ((lz4_ms + gather_ms) / 1e3) / 1e9, 3)),
         "value_per_gpu": round(lz4_gbs / world, 3),

@@ -194,7 +194,12 @@ int lz4r_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap,
  * beside LZ4R_LEN_CORRUPT of the call's length word (so the caller's length
  * buffer may already be freed).  Every call folds the kernel's status into
  * its own length word and clears it, so an async caller that reads the
- * length needs no separate check.  lz4r_compress_device checks by itself. */
+ * length needs no separate check.  lz4r_compress_device checks by itself.
+ * Ordering: the verdict word is one per context and every call overwrites it,
+ * whatever stream that call runs on.  Pass the stream the compress call ran
+ * on, and call lz4r_check before the next compress call on this context;
+ * otherwise the word read is unordered with, or belongs to, another call
+ * (the length word's bit 63 has no such restriction). */
 int lz4r_check(lz4r_ctx *ctx, void *stream);
 
 /* Measurement: when enabled, every compress call records HIP events on its

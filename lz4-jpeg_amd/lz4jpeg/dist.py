@@ -10,8 +10,9 @@ assembly of the framed stream:
   1. all_gather of one int64 segment length per rank -> exclusive offsets
      (every rank then knows where its segment lands in the global stream);
   2. gatherv of the segments to the destination rank as batched P2P
-     send/recv (segment sizes differ, so no padded gather), which writes the
-     frame header byte u8(total_blocks) in front (write_output, LZ4.c:429).
+     send/recv in rounds of <= 1 GiB pieces (segment sizes differ, so no
+     padded gather), which writes the frame header byte u8(total_blocks) in
+     front (write_output, LZ4.c:429).
 Concatenation is exact because a block's bytes depend only on that block.
 
 The JPEG path shards images (or tile rows) with no exchange at all.
@@ -59,42 +60,67 @@ def exchange_lengths(seg_len, device, group=None):
     return lens, offs
 
 
-def gather_stream(segment, seg_len, nb_total, lens, offs, dst=0, group=None):
+# Largest single P2P message of the gatherv.  An 8-GPU config-4 segment is
+# ~8.9 GB; one isend of that size has never run on RCCL, so every segment
+# moves as a sequence of <= 1 GiB send/recv pairs.
+GATHER_CHUNK = 1 << 30
+
+
+def chunk_ranges(length, chunk=GATHER_CHUNK):
+    """[(lo, hi), ...] cutting [0, length) into pieces of at most `chunk` bytes."""
+    if chunk <= 0:
+        raise ValueError("chunk must be positive")
+    return [(lo, min(lo + chunk, length)) for lo in range(0, length, chunk)]
+
+
+def gather_stream(segment, seg_len, nb_total, lens, offs, dst=0, group=None,
+                  chunk=GATHER_CHUNK):
     """Assemble [u8 nb_total] + seg_0 + ... + seg_{W-1} on rank `dst`.
     `segment` is this rank's uint8 tensor (at least seg_len bytes) on the
-    backend's device.  Returns the framed stream tensor on dst, None elsewhere."""
+    backend's device.  Returns the framed stream tensor on dst, None elsewhere.
+
+    The gatherv runs in rounds: round k moves the k-th <= `chunk`-byte piece
+    of every segment that has one, as one batched P2P group, and waits for it
+    before the next round -- so no message exceeds `chunk` bytes and at most
+    one piece per sender is in flight.  Every rank derives the same round
+    count from `lens` (the all_gather'ed lengths), so sends and receives pair
+    up round by round; empty segments take part in no round."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
+    pieces = [chunk_ranges(L, chunk) for L in lens]
+    rounds = max((len(p) for r, p in enumerate(pieces) if r != dst), default=0)
+    out = None
     if rank == dst:
         total = 1 + sum(lens)
         out = torch.empty(total, dtype=torch.uint8, device=segment.device)
         out[0] = nb_total & 0xFF
         out[1 + offs[rank]:1 + offs[rank] + seg_len].copy_(segment[:seg_len])
+    for k in range(rounds):
         ops = []
-        for r in range(world):
-            if r == dst or lens[r] == 0:
-                continue
-            view = out[1 + offs[r]:1 + offs[r] + lens[r]]
-            ops.append(dist.P2POp(dist.irecv, view, r, group=group))
+        if rank == dst:
+            for r in range(world):
+                if r == dst or k >= len(pieces[r]):
+                    continue
+                lo, hi = pieces[r][k]
+                view = out[1 + offs[r] + lo:1 + offs[r] + hi]
+                ops.append(dist.P2POp(dist.irecv, view, r, group=group))
+        elif k < len(pieces[rank]):
+            lo, hi = pieces[rank][k]
+            ops.append(dist.P2POp(dist.isend, segment[lo:hi].contiguous(), dst, group=group))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
-        return out
-    if seg_len > 0:
-        op = dist.P2POp(dist.isend, segment[:seg_len].contiguous(), dst, group=group)
-        for req in dist.batch_isend_irecv([op]):
-            req.wait()
-    return None
+    return out
 
 
-def compress_sharded(local, n_total, compress_segment, dst=0, group=None):
+def compress_sharded(local, n_total, compress_segment, dst=0, group=None, chunk=GATHER_CHUNK):
     """Full sharded job on this rank's slice `local` (uint8 tensor of
     shard_bytes(n_total, W, rank)).  `compress_segment(tensor) -> (out, len)`
     is the per-rank compressor (the HIP path in production; tests may pass a
     CPU checker).  Returns the framed stream on dst, None elsewhere."""
     seg, seg_len = compress_segment(local)
     lens, offs = exchange_lengths(seg_len, seg.device, group)
-    return gather_stream(seg, seg_len, nblocks(n_total), lens, offs, dst, group)
+    return gather_stream(seg, seg_len, nblocks(n_total), lens, offs, dst, group, chunk)
 
 
 def hip_segment_compressor(compressor, final_shard, stream=None):

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, data, expect, q):
+def _worker(rank, world, port, data, expect, q, chunk=ldist.GATHER_CHUNK):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "lz4-jpeg_amd"))
     import oracle_api
@@ -44,23 +44,32 @@ def _worker(rank, world, port, data, expect, q):
             out = o.lz4_blocks(b, 0, nb)
             return torch.from_numpy(np.frombuffer(out, dtype=np.uint8).copy()), len(out)
 
-        got = d.compress_sharded(local, n, seg, dst=0)
+        got = d.compress_sharded(local, n, seg, dst=0, chunk=chunk)
         if rank == 0:
             q.put(bytes(got.numpy().tobytes()) == expect)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 300 * 41 + 17), (2, 300 * 40), (3, 300 * 7 + 1),
-                                     (2, 300 * 3)])
-def test_sharded_stream_equals_single(oracle, world, n):
+@pytest.mark.parametrize("world,n,chunk", [
+    (2, 300 * 41 + 17, ldist.GATHER_CHUNK), (2, 300 * 40, ldist.GATHER_CHUNK),
+    (3, 300 * 7 + 1, ldist.GATHER_CHUNK), (2, 300 * 3, ldist.GATHER_CHUNK),
+    # config 4's world size: uneven segments (41 or 42 blocks of differing
+    # compressibility), gathered in 1 KiB pieces, i.e. 3-4 rounds per sender
+    (8, 300 * 333 + 17, 1024),
+    # more ranks than blocks: ranks 0 (the destination) and 4 hold empty shards
+    # (no rounds) while the others send two pieces each
+    (8, 300 * 5 + 1, 256),
+    # a chunk that divides a segment exactly is one more edge of the rounds
+    (8, 300 * 64, 100)])
+def test_sharded_stream_equals_single(oracle, world, n, chunk):
     import golden_inputs
     data = golden_inputs.lz4_input("metamorphosis_spaces")[:n]
     expect = oracle.lz4_compress(data)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, data, expect, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, expect, q, chunk))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -125,3 +134,15 @@ def test_shards_are_block_aligned_and_cover():
                 assert hi == n or hi % 300 == 0
                 prev = hi
             assert prev == n
+
+
+def test_chunk_ranges():
+    assert ldist.chunk_ranges(0, 4) == []
+    assert ldist.chunk_ranges(8, 4) == [(0, 4), (4, 8)]
+    assert ldist.chunk_ranges(9, 4) == [(0, 4), (4, 8), (8, 9)]
+    big = 9_000_000_000                    # an 8-GPU config-4 segment
+    r = ldist.chunk_ranges(big)
+    assert len(r) == 9 and r[-1][1] == big
+    assert all(hi - lo <= 1 << 30 for lo, hi in r)
+    with pytest.raises(ValueError):
+        ldist.chunk_ranges(10, 0)
