@@ -53,6 +53,12 @@ __constant__ int dZZ8b[64];     // 2 * zigzag position: the int16's byte offset 
 __constant__ int dZZ4b[32];
 __constant__ int dZZ8inv[64];   // zigzag index -> natural index
 __constant__ int dZZ4inv[32];
+// reconstruction, per position z of a tile's 128 zigzagged int16 ([Y 64][Cr 32][Cb 32]):
+// the natural index within its plane, the quantiser step and the alpha product
+// of that index -- one load each, none depending on another
+__constant__ int dRZn[128];
+__constant__ double dRZq[128];
+__constant__ double dRZa[128];
 
 __device__ __forceinline__ int clamp_u8(int v) {       // JPEG.c:132-139
   return v < 0 ? 0 : (v > 255 ? 255 : v);
@@ -291,6 +297,27 @@ __global__ __launch_bounds__(kEThreads) void jpeg_strip_kernel(
   }
 }
 
+// (int)round(x) clamped to 0..255 (JPEG.c:440-446).  round() is half away
+// from zero; for x >= 0 that is trunc(x) + (x - trunc(x) >= 0.5), the
+// fraction exact in fp64.  A negative x clamps to 0 either way (trunc
+// toward zero gives <= 0 there), as does anything at or past 255.5.
+__device__ __forceinline__ int round_clamp_u8(double x) {
+  const int i = (int)x;                          // v_cvt_i32_f64: toward zero, saturating
+  const int v = i + ((x - (double)i) >= 0.5 ? 1 : 0);
+  return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// The colour terms of assemble_image (JPEG.c:601-603): (int)(k * (double)d)
+// for d = Cr - 128 or Cb - 128 in -128..127 and k in {1.402, 0.344136,
+// 0.714136, 1.772}.  k d is never within 0.00104 of a nonzero integer on that
+// range (k = m / 10^e with d m not a multiple of 10^e unless d = 0), and the
+// fp64 product is within 1e-13 of k d, so its truncation is trunc(k d); the
+// fp32 product of the rounded k is within 3e-5 of k d, so it truncates the
+// same way.  Checked for all 4 x 256 cases by tests/test_tables.py.
+__device__ __forceinline__ int colour_term(float k, int d) {
+  return (int)(k * (float)d);
+}
+
 // ---- reconstruction: the decode side of the reference's main --------------
 // (JPEG.c:1131-1425 minus the entropy round trip, which is the identity on
 // the coefficients): per tile, reverse zigzag + Inverse_quantize (:631-638),
@@ -330,19 +357,15 @@ __global__ __launch_bounds__(kThreads) void jpeg_recon_kernel(
     const int stride = luma ? kYStride : kCStride;
     int nat[8];
     double qs[8], aa[8];
+    // one load each from z-indexed tables, none depending on another (a
+    // zigzag -> natural lookup followed by the step / alpha loads it indexes
+    // was two dependent memory round trips at the head of every workgroup:
+    // 74.4 -> 64.5 us per 4K image, tools/ab_recon_inproc.py)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (luma) {
-        const int n8 = dZZ8inv[z0 + j];
-        nat[j] = n8;
-        qs[j] = (double)dLQ[n8];
-        aa[j] = dAA88[n8 >> 3][n8 & 7];
-      } else {
-        const int n4 = dZZ4inv[(z0 + j - 64) & 31];
-        nat[j] = n4;
-        qs[j] = (double)dCQ[n4];
-        aa[j] = dAA84[n4 >> 2][n4 & 3];
-      }
+      nat[j] = dRZn[z0 + j];
+      qs[j] = dRZq[z0 + j];
+      aa[j] = dRZa[z0 + j];
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -381,10 +404,8 @@ __global__ __launch_bounds__(kThreads) void jpeg_recon_kernel(
         }
       }
 #pragma unroll
-      for (int y = 0; y < 8; ++y) {
-        const int value = (int)round(s[y] + 128.0);                      // JPEG.c:440
-        ys[tile * 64 + x * 8 + y] = (uint8_t)(value < 0 ? 0 : (value > 255 ? 255 : value));
-      }
+      for (int y = 0; y < 8; ++y)
+        ys[tile * 64 + x * 8 + y] = (uint8_t)round_clamp_u8(s[y] + 128.0);   // JPEG.c:440
     }
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
@@ -403,10 +424,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_recon_kernel(
       }
       uint8_t *dst = (ch == 0 ? crs : cbs) + tile * 32 + x * 4;
 #pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        const int value = (int)round(s[y] + 128.0);
-        dst[y] = (uint8_t)(value < 0 ? 0 : (value > 255 ? 255 : value));
-      }
+      for (int y = 0; y < 4; ++y) dst[y] = (uint8_t)round_clamp_u8(s[y] + 128.0);
     }
   }
   __syncthreads();
@@ -448,10 +466,10 @@ __global__ __launch_bounds__(kThreads) void jpeg_recon_kernel(
             Cr = crs[tile * 32 + r * 4 + (col >> 1)];
             Cb = cbs[tile * 32 + r * 4 + (col >> 1)];
           }
-          const int R = Y + (int)(1.402 * (double)(Cr - 128));              // JPEG.c:601
-          const int G = Y - (int)(0.344136 * (double)(Cb - 128)) -
-                        (int)(0.714136 * (double)(Cr - 128));
-          const int B = Y + (int)(1.772 * (double)(Cb - 128));
+          const int R = Y + colour_term(1.402f, Cr - 128);            // JPEG.c:601
+          const int G = Y - colour_term(0.344136f, Cb - 128) -
+                        colour_term(0.714136f, Cr - 128);
+          const int B = Y + colour_term(1.772f, Cb - 128);
           px[k] = (uint32_t)clamp_u8(R) | ((uint32_t)clamp_u8(G) << 8) |
                   ((uint32_t)clamp_u8(B) << 16) | (255u << 24);
         }
@@ -501,6 +519,24 @@ hipError_t upload_tables() {
   for (int i = 0; i < 32; ++i) i4[ZZ4_POS[i]] = i;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ8inv), i8, sizeof(i8))) != hipSuccess) return e;
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dZZ4inv), i4, sizeof(i4))) != hipSuccess) return e;
+  int rzn[128];
+  double rzq[128], rza[128];
+  for (int z = 0; z < 128; ++z) {
+    if (z < 64) {
+      const int n = i8[z];
+      rzn[z] = n;
+      rzq[z] = (double)lq[n];
+      rza[z] = AA88[n >> 3][n & 7];
+    } else {
+      const int n = i4[(z - 64) & 31];
+      rzn[z] = n;
+      rzq[z] = (double)cq[n];
+      rza[z] = AA84[n >> 2][n & 3];
+    }
+  }
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dRZn), rzn, sizeof(rzn))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dRZq), rzq, sizeof(rzq))) != hipSuccess) return e;
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(dRZa), rza, sizeof(rza))) != hipSuccess) return e;
   if (dev >= 0 && dev < 64) g_tables_ready[dev] = true;
   return hipSuccess;
 }

@@ -829,29 +829,38 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
   if constexpr (!kLuma) {
     // Deferred streams (a symbol outside the table or more than Cap
     // distinct): the hashed encoder over this wave's LDS, which the fast path
-    // has left dead, one stream at a time on lane 0 -- the wave's own, then
-    // (an even wave) those of luma wave lv, whose overflowed lanes it counts.
+    // has left dead -- the wave's own, then (an even wave) those of luma wave
+    // lv, whose overflowed lanes it counts.  The dead LDS holds kSlots
+    // working sets, so lanes 0 .. kSlots-1 each take every kSlots-th stream
+    // of the list (a 4K image whose every luma stream defers: 15.97 ms with
+    // one lane, 2.50 ms with 6; profiles/r06_ent_defer_defer_y.log).
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    if (lane == 0) {
-      const uint32_t lw = (blockIdx.x & 1) ? 0u : *lword;
-      if (lw >> 8) atomicAdd(&status[0], lw >> 8);
-      constexpr int kSymO = 0, kHashO = kSymO + 2 * kFullCap, kHeapO = kHashO + 2 * kFullCap;
-      constexpr int kCodeO = (kHeapO + 2 * (kFullCap + 2) + 3) & ~3, kLenO = kCodeO + 4 * kFullCap;
-      constexpr int kStkO = (kLenO + kFullCap + 1) & ~1, kEnd = kStkO + 2 * (kFullCap + 1);
-      static_assert(kEnd <= (int)sizeof(L), "the hashed encoder's arrays fit the wave's LDS");
-      uint8_t *const lb = reinterpret_cast<uint8_t *>(&S);
+    constexpr int kSymO = 0, kHashO = kSymO + 2 * kFullCap, kHeapO = kHashO + 2 * kFullCap;
+    constexpr int kCodeO = (kHeapO + 2 * (kFullCap + 2) + 3) & ~3, kLenO = kCodeO + 4 * kFullCap;
+    constexpr int kStkO = (kLenO + kFullCap + 1) & ~1, kEnd = kStkO + 2 * (kFullCap + 1);
+    constexpr int kSetB = (kEnd + 15) & ~15;                // one working set, 16-B aligned
+    constexpr int kSlots = (int)sizeof(L) / kSetB < 8 ? (int)sizeof(L) / kSetB : 8;
+    static_assert(kSlots >= 1, "the hashed encoder's arrays fit the wave's LDS");
+    const uint32_t lw = (blockIdx.x & 1) ? 0u : *lword;
+    const int nown = __popcll(dm), n = nown + (int)(lw & 255u);
+    if (lane == 0 && (lw >> 8)) atomicAdd(&status[0], lw >> 8);
+    // (the last wave's lanes past ntiles have returned: only live lanes take a share)
+    const int nlive = (int)min((size_t)kLanes, ntiles - lv * kLanes);
+    const int slots = kSlots < nlive ? kSlots : nlive;
+    if (lane < slots && lane < n) {
+      uint8_t *const lb = reinterpret_cast<uint8_t *>(&S) + lane * kSetB;
       const Work<GColT> ws{{reinterpret_cast<int16_t *>(lb + kSymO), 1}, {lb + kHashO, 1},
                            {reinterpret_cast<uint16_t *>(lb + kHeapO), 1},
                            {reinterpret_cast<uint32_t *>(lb + kCodeO), 1}, {lb + kLenO, 1},
                            {reinterpret_cast<uint16_t *>(lb + kStkO), 1}};
-      const int nown = __popcll(dm), n = nown + (int)(lw & 255u);
-      uint64_t own = dm;
-      for (int k = 0; k < n; ++k) {
+      uint64_t own = dm;                              // the wave's own deferred lanes, in order
+      for (int j = 0; j < lane && own; ++j) own &= own - 1;
+      for (int k = lane; k < n; k += slots) {
         uint32_t sid;                                 // tile * 3 + channel
         if (k < nown) {
           sid = (uint32_t)((lv * kLanes + __builtin_ctzll(own)) * 3 + c);
-          own &= own - 1;
+          for (int j = 0; j < slots && own; ++j) own &= own - 1;
         } else {
           sid = lst[k - nown];
         }

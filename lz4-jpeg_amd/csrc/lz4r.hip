@@ -1411,7 +1411,10 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
 // scan -> gather pass that continues the stream offset the previous chunk
 // left in *d_len; the per-chunk launch cost (four launches) is noise against
 // the ~19 ms of encoder work in a full chunk.
-constexpr size_t kChunk = size_t(1) << 24;
+#ifndef LZ4R_CHUNK_LOG2
+#define LZ4R_CHUNK_LOG2 24
+#endif
+constexpr size_t kChunk = size_t(1) << LZ4R_CHUNK_LOG2;
 static_assert(kChunk % kPart == 0, "chunks start on a scan partial");
 static_assert((kChunk / 8) * 8 * 64 < (size_t(1) << 32), "chunk grid fits HIP's limit");
 // largest input one call accepts (block indices are u32 in the per-call arrays)

@@ -46,3 +46,42 @@ def test_zigzag_chroma_order():
         order[k] = i
     assert order == [0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 16, 13, 10, 7, 11, 14, 17, 20, 24, 21, 18,
                      15, 19, 22, 25, 28, 29, 26, 23, 27, 30, 31]
+
+
+def test_colour_terms_fp32_equal_fp64():
+    """jpeg_recon_kernel's colour terms (assemble_image, JPEG.c:598-600): the
+    truncation of the fp32 product fl32(k) * d equals the reference's (int) of
+    the fp64 product k * (double)d for every d = Cr - 128 / Cb - 128 in
+    -128..127 and each of the four constants, and no product lies within
+    0.001 of a nonzero integer (the margin the kernel's comment relies on)."""
+    import numpy as np
+    d = np.arange(-128, 128)
+    for k in (1.402, 0.344136, 0.714136, 1.772):
+        ref = np.trunc(k * d.astype(np.float64)).astype(np.int64)
+        f32 = np.trunc(np.float32(k) * d.astype(np.float32)).astype(np.int64)
+        assert np.array_equal(ref, f32), k
+        x = k * d[d != 0]
+        assert np.min(np.abs(x - np.round(x))) > 0.001, k
+
+
+def test_round_clamp_by_truncation():
+    """round_clamp_u8 (jpeg_recon_kernel): (int)round(x) clamped to 0..255
+    (JPEG.c:440-446) equals trunc + (fraction >= 0.5) clamped, on the values
+    where the two could differ: halves, their neighbours, negatives, and
+    values past 255."""
+    import numpy as np
+    xs = []
+    for k in range(-3, 259):
+        for off in (-0.5, 0.0, 0.5):
+            b = k + off
+            xs += [b, np.nextafter(b, -1e9), np.nextafter(b, 1e9)]
+    xs += list(np.random.default_rng(1).uniform(-300, 600, 20000))
+    from decimal import ROUND_HALF_UP, Decimal
+    for x in xs:
+        x = float(x)
+        # C round(): half away from zero, on the exact binary value
+        v = int(Decimal(x).quantize(Decimal(1), rounding=ROUND_HALF_UP))
+        ref = min(255, max(0, v))
+        i = int(x)                                   # toward zero, as v_cvt_i32_f64
+        got = min(255, max(0, i + (1 if x - i >= 0.5 else 0)))
+        assert got == ref, x

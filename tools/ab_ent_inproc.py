@@ -7,7 +7,14 @@ ctypes handle, RTLD_LOCAL) encodes them with jpegr_entropy_encode_device,
 round-robin after 100 ms of warm-up; per call torch events on the current
 stream; then each build decodes its own encoding (jpegr_entropy_decode_device,
 timed the same way).  Every build's bits / meta / table / status are compared
-with the first build's, and every decode with the coefficients."""
+with the first build's, and every decode with the coefficients.
+
+ENT_COEF=rand (default) | defer_y | defer_all: the coefficients.  defer_y
+gives every luma stream 64 distinct values (a per-tile permutation of
+-32..31: 65 distinct RLE symbols, past the 24 of the direct table), so every
+luma stream of every wave is deferred to the hashed encoder (the
+worst case of the deferred path); defer_all does the same to both chroma
+streams (-16..15)."""
 import ctypes
 import os
 import statistics
@@ -31,8 +38,20 @@ def main():
     d_img = torch.from_numpy(synth.rand_rgba(W, H, seed=1)).cuda()
     d_coef = jpeg.encode_device(d_img, W, H)
     nt = jpeg.tiles(W, H)
-    libs[0].jpegr_entropy_scratch_bytes.restype = ctypes.c_size_t
-    sb = libs[0].jpegr_entropy_scratch_bytes(ctypes.c_size_t(nt))
+    mode = os.environ.get("ENT_COEF", "rand")
+    if mode != "rand":
+        g = torch.Generator(device="cuda").manual_seed(7)
+        c = d_coef.view(nt, 128)
+        c[:, :64] = (torch.argsort(torch.rand(nt, 64, device="cuda", generator=g), dim=1) - 32).to(torch.int16)
+        if mode == "defer_all":
+            for lo in (64, 96):
+                c[:, lo:lo + 32] = (torch.argsort(torch.rand(nt, 32, device="cuda", generator=g),
+                                                  dim=1) - 16).to(torch.int16)
+    print("coefficients:", mode, flush=True)
+    sb = 0
+    for lib in libs:
+        lib.jpegr_entropy_scratch_bytes.restype = ctypes.c_size_t
+        sb = max(sb, lib.jpegr_entropy_scratch_bytes(ctypes.c_size_t(nt)))
     outs = []
     for _ in libs:
         outs.append(dict(bits=torch.zeros(nt * 256, dtype=torch.uint8, device="cuda"),
