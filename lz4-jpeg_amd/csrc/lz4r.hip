@@ -158,10 +158,7 @@ static_assert(kInOff + kBlk + 48 <= kQOff && kQOff % 16 == 0 && kInOff % 16 == 0
 // reads its 32 blocks' heads as one contiguous 3 KB run of 16-B loads (no
 // 128-B line per block of which ~60 B were used); records 23.. go to a
 // per-block overflow slot of kOvf bytes.
-#ifndef LZ4R_HEADW
-#define LZ4R_HEADW 24
-#endif
-constexpr int kHeadW = LZ4R_HEADW;
+constexpr int kHeadW = 24;
 constexpr int kHead = 4 * kHeadW;        // 96 B
 constexpr int kOvf = 400;                // records 23..120: <= 98 dwords
 constexpr int kSlot = kHead + kOvf;      // scratch bytes per block
@@ -1150,7 +1147,7 @@ __device__ __forceinline__ void or_bytes(uint32_t *buf32, int x, uint32_t v) {
   atomicOr(&buf32[(x >> 2) + 1], (uint32_t)(w >> 32));
 }
 
-// Records -> bytes of one emit task (lz4_emit, lz4_emit_p): wave wv takes
+// Records -> bytes of one emit task (lz4_emit): wave wv takes
 // blocks [h0 + 4 wv, ...) of the task's [h0, h1); the image img[lead] is
 // stream byte G0; block h's input is stage[kStagePad + 300 (h - h0) + p].
 __device__ __forceinline__ void emit_records(const int wv, const int lane, const int h0,
@@ -1434,197 +1431,6 @@ __global__ __launch_bounds__(64 * kEW) void lz4_emit(
   emit_store(tid, wv, lane, G0, min(toff[h1], cap), lead, img, out);
 }
 
-// ---- lz4_emit_p: lz4_emit as a persistent, prefetching loop -----------------
-// lz4_emit's workgroup loads its task, waits, computes, stores: the ablations
-// (tools/r06_g.sh) put the loads + stores alone at 0.41 ms per GiB (6.1 TB/s)
-// and the whole kernel at 0.60 -- the records -> bytes phase does not overlap
-// the memory traffic.  Here a workgroup walks a list of tasks and, before it
-// waits for task k's data, issues task k + 1's loads straight into a second
-// set of LDS buffers (global_load_lds_dwordx4: no VGPRs), so the next task's
-// loads are in flight through the whole of task k's compute and stores.  Every
-// load of the loop is an LDS-DMA issued by a fixed set of waves, so each wave
-// waits for exactly the loads older than its prefetch (s_waitcnt vmcnt(N): the
-// VM counter retires loads, stores and LDS-DMA in issue order) and the
-// barriers are raw s_barriers (__syncthreads' fence would drain the prefetch).
-// The input must be 16-B aligned (the host falls back to lz4_emit).
-constexpr int kPStage = kStagePad + 16 * 640 + 32;   // the DMA rounds cover chunks 0..639
-constexpr int kPHeadB = 4096;                        // heads: four waves' DMA of 1 KB
-static_assert(kGH * kHead <= kPHeadB && kGH * kBlk / 16 <= 640, "DMA rounds cover a task");
-struct EmitPLds {
-  alignas(16) uint8_t stage[2][kPStage];
-  alignas(16) uint8_t recst[2][kPHeadB];             // [kGH][kRecPre] dwords + DMA overshoot
-  alignas(16) uint32_t scan[2][192];                 // gsum[64] | tsz[64] | part (2 dwords)
-  alignas(16) uint8_t img[kEmitImg];
-  uint64_t toff[kGT + 1];
-  uint32_t marks[kEW][64];
-  uint4 pmask[17];
-};
-
-struct EmitTask {
-  size_t g, g0, b0;
-  int h0, h1, nt, len, n16;
-};
-
-// task wg of an emit launch (lz4_emit's mapping); false when it holds no block
-__device__ __forceinline__ bool emit_task(uint32_t wg, uint32_t nwg, size_t ntiles, size_t g_first,
-                                          uint64_t nb_total, uint32_t last_n, EmitTask &T) {
-  if (wg >= nwg) return false;
-  T.g = g_first + wg / kGSplit;
-  T.h0 = (int)(wg % kGSplit) * kGH;
-  T.g0 = T.g * kGT;
-  T.nt = (int)min((size_t)kGT, ntiles - T.g0);
-  if (T.h0 >= T.nt) return false;
-  T.h1 = min(T.nt, T.h0 + kGH);
-  T.b0 = T.g0 + T.h0;
-  T.len = (T.h1 - T.h0 - 1) * kBlk + (T.g0 + T.h1 == nb_total ? (int)last_n : kBlk);
-  T.n16 = T.len >> 4;
-  return true;
-}
-
-// global -> LDS DMA of 16 (4) bytes per lane: lane l's bytes at base + off_l
-// land at LDS byte m0 + 16 l (4 l), m0 = the wave's destination.  Inline asm,
-// so that the compiler does not know the LDS writes are in flight: for the
-// builtin it waits vmcnt(0) before every later LDS access (it cannot tell the
-// two buffer sets apart), which drains the prefetch; the kernel waits for the
-// DMA itself (emit_wait).  m0 is written only here in lz4_emit_p.
-__device__ __forceinline__ uint32_t lds_off(const void *p) {   // (wave-uniform by construction)
-  return (uint32_t)__builtin_amdgcn_readfirstlane(
-      (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void *)p);
-}
-__device__ __forceinline__ void glds16(const void *base, uint32_t off, const void *lds_wave) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-               :
-               : "v"(off), "s"(base), "s"(lds_off(lds_wave))
-               : "memory");
-}
-__device__ __forceinline__ void glds4(const void *base, uint32_t off, const void *lds_wave) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
-               :
-               : "v"(off), "s"(base), "s"(lds_off(lds_wave))
-               : "memory");
-}
-
-// Task T's loads into buffer set b, as LDS-DMA.  Per wave a fixed count
-// (emit_wait): the input's 16-B chunks in two rounds (chunk 64 wv + lane, then
-// 512 + 64 wv + lane on waves 0-1), the record heads on waves 0-3, the scan
-// inputs on waves 4 (group sums), 5 (block sizes) and 6 (the partial).
-// Lanes past the data load a valid dummy address into LDS nobody reads.
-__device__ __forceinline__ void emit_prefetch(const EmitTask &T, EmitPLds &S, int b, int wv,
-                                              int lane, const uint8_t *in,
-                                              const uint8_t *heads, size_t slot_base,
-                                              const uint32_t *tsz, const uint32_t *gsum,
-                                              const uint64_t *part) {
-  const uint8_t *src = in + T.b0 * kBlk;
-  {
-    const int i = 64 * wv + lane;
-    glds16(src, 16u * (uint32_t)(i < T.n16 ? i : 0), &S.stage[b][kStagePad + 1024 * wv]);
-  }
-  if (wv < 2) {
-    const int i = 512 + 64 * wv + lane;
-    glds16(src, 16u * (uint32_t)(i < T.n16 ? i : 0), &S.stage[b][kStagePad + 16 * 512 + 1024 * wv]);
-  }
-  if (wv < 4) {
-    const uint8_t *wh = heads + (T.b0 - slot_base) * (size_t)kHead;
-    const int j = 64 * wv + lane;
-    glds16(wh, 16u * (uint32_t)(j < (T.h1 - T.h0) * (kHead / 16) ? j : 0), &S.recst[b][1024 * wv]);
-  } else if (wv == 4) {
-    const size_t gfirst = (T.g0 / kPart) * 64;       // first group of the partial (<= g)
-    glds4(gsum + gfirst, 4u * (uint32_t)(gfirst + (size_t)lane < T.g ? lane : 0), &S.scan[b][0]);
-  } else if (wv == 5) {
-    glds4(tsz + T.g0, 4u * (uint32_t)(lane < T.nt ? lane : 0), &S.scan[b][64]);
-  } else if (wv == 6) {
-    glds4(part + T.g0 / kPart, 4u * (uint32_t)(lane & 1), &S.scan[b][128]);
-  }
-}
-
-// wait for everything but this wave's prefetch (emit_prefetch's count)
-__device__ __forceinline__ void emit_wait(int wv, bool prefetched) {
-  if (!prefetched) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else if (wv < 2) {
-    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  } else if (wv < 7) {
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  }
-}
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-__global__ __launch_bounds__(64 * kEW) __attribute__((amdgpu_waves_per_eu(6, 8))) void lz4_emit_p(
-    const uint8_t *__restrict__ in, const uint8_t *__restrict__ heads,
-    const uint8_t *__restrict__ ovfs, size_t slot_base,
-    const uint32_t *__restrict__ tsz, size_t ntiles, size_t g_first,
-    const uint32_t *__restrict__ gsum, const uint64_t *__restrict__ part,
-    uint8_t *__restrict__ out, uint64_t cap, int hdr, uint64_t nb_total, uint32_t last_n,
-    uint64_t *__restrict__ boff) {
-  __shared__ EmitPLds S;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // lz4_emit's XCD-aware task order: XCD x takes tasks [x per, (x + 1) per);
-  // its workgroups (b, b + 8, ...) walk that range in steps of their count
-  const uint32_t nwg = (uint32_t)((ntiles - g_first * kGT + kGT - 1) / kGT) * kGSplit;
-  const uint32_t per = (nwg + 7) / 8;
-  const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
-  auto task = [&](uint32_t k, EmitTask &T) {
-    const uint32_t s = slot + k * nslot;
-    return s < per && emit_task(xcd * per + s, nwg, ntiles, g_first, nb_total, last_n, T);
-  };
-  EmitTask T;
-  bool have = task(0, T);
-  if (!have) return;
-  if (tid < 17) {
-    uint32_t m[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = min(max(tid - 4 * j, 0), 4);
-      m[j] = n == 4 ? ~0u : (1u << (8 * n)) - 1u;
-    }
-    S.pmask[tid] = make_uint4(m[0], m[1], m[2], m[3]);
-  }
-  emit_prefetch(T, S, 0, wv, lane, in, heads, slot_base, tsz, gsum, part);
-  for (uint32_t k = 0; have; ++k) {
-    const int cb = (int)(k & 1u);
-    EmitTask Tn;
-    const bool nxt = task(k + 1, Tn);
-    if (nxt) emit_prefetch(Tn, S, cb ^ 1, wv, lane, in, heads, slot_base, tsz, gsum, part);
-    emit_wait(wv, nxt);
-    raw_barrier();                                   // task k's data is in S.*[cb]
-    if (wv == 0) {
-      __builtin_amdgcn_s_setprio(3);
-      const size_t gfirst = (T.g0 / kPart) * 64;
-      const uint32_t gs = gfirst + (size_t)lane < T.g ? S.scan[cb][lane] : 0u;
-      const uint32_t tv = lane < T.nt ? S.scan[cb][64 + lane] : 0u;
-      const uint64_t pt = (uint64_t)S.scan[cb][128] | (uint64_t)S.scan[cb][129] << 32;
-      const uint64_t base = pt + lane63(wave_incl_add(gs));
-      const uint32_t inc = wave_incl_add(tv);
-      S.toff[lane] = base + inc - tv;
-      if (lane == 63) S.toff[kGT] = base + inc;
-      if (T.h0 == 0 && lane < T.nt) boff[T.g0 + lane] = base + inc - tv - (uint64_t)hdr;
-      if (hdr && T.g == 0 && T.h0 == 0 && lane == 0 && cap > 0) out[0] = (uint8_t)nb_total;
-    }
-    for (int i = tid; i < kEmitImg / 16; i += 64 * kEW)
-      reinterpret_cast<uint4 *>(S.img)[i] = make_uint4(0, 0, 0, 0);
-    if (T.len > 16 * T.n16) {                        // the call's last task: its short tail
-      const uint8_t *src = in + T.b0 * kBlk;
-      for (int i = 16 * T.n16 + tid; i < T.len; i += 64 * kEW) S.stage[cb][kStagePad + i] = src[i];
-    }
-    raw_barrier();
-    if (wv == 0) __builtin_amdgcn_s_setprio(0);
-    const uint64_t G0 = S.toff[T.h0];
-    const int lead = (int)(((uintptr_t)out + G0) & 15);
-    emit_records(wv, lane, T.h0, T.h1, G0, lead, S.toff, S.img, S.stage[cb],
-                 reinterpret_cast<const uint32_t (*)[kRecPre]>(&S.recst[cb][0]), S.marks, S.pmask,
-                 ovfs + (T.b0 - slot_base) * (size_t)kOvf);
-    raw_barrier();
-    emit_store(tid, wv, lane, G0, min(S.toff[T.h1], cap), lead, S.img, out);
-    T = Tn;
-    have = nxt;
-  }
-}
-
 }  // namespace
 
 // Launch chunking: lz4_tiles is a 64-lane workgroup per block, and a HIP
@@ -1636,10 +1442,6 @@ __global__ __launch_bounds__(64 * kEW) __attribute__((amdgpu_waves_per_eu(6, 8))
 // scan -> gather pass that continues the stream offset the previous chunk
 // left in *d_len; the per-chunk launch cost (four launches) is noise against
 // the ~19 ms of encoder work in a full chunk.
-// lz4_emit as the persistent, prefetching lz4_emit_p (tools A/B until measured)
-#ifndef LZ4R_EMIT_PERSIST
-#define LZ4R_EMIT_PERSIST 0
-#endif
 #ifndef LZ4R_CHUNK_LOG2
 #define LZ4R_CHUNK_LOG2 24
 #endif
@@ -1651,7 +1453,6 @@ constexpr size_t kMaxInput = size_t(1) << 40;
 
 struct lz4r_ctx {
   int device = 0;
-  int ncu = 256;               // compute units (the persistent emit's grid)
   size_t cap_blocks = 0;       // capacity of the per-call per-block arrays
   size_t cap_slots = 0;        // capacity of the slot scratch, in blocks (<= kChunk)
   uint16_t *bsizes = nullptr;  // encoded bytes of every block of the last call
@@ -1825,18 +1626,6 @@ int run(lz4r_ctx *c, const void *d_in, size_t n, void *d_out, size_t cap,
                        (uint64_t)hdr, k == 0 ? 1 : 0, k + 1 == nchunks ? 1 : 0, c->status,
                        static_cast<uint64_t *>(d_len), c->verdict);
     const size_t g0 = b0 / kGT, ng = (nbc + kGT - 1) / kGT;
-    const unsigned nwg_e = (unsigned)(8 * ((ng * kGSplit + 7) / 8));
-    if (LZ4R_EMIT_PERSIST && (((uintptr_t)in & 15) == 0)) {
-      // three workgroups per CU (49 KB of LDS each), each walking its tasks
-      const unsigned grid_p = std::min(nwg_e, (unsigned)(8 * ((3 * c->ncu + 7) / 8)));
-      hipExtLaunchKernelGGL(lz4_emit_p, dim3(grid_p), dim3(64 * kEW), 0, s, nullptr,
-                            k + 1 == nchunks ? ev(ts ? ts->c : nullptr) : nullptr, 0u, in,
-                            (const uint8_t *)c->slots, (const uint8_t *)ovfs, b0,
-                            (const uint32_t *)c->tsz, b1, g0, (const uint32_t *)c->gsum,
-                            (const uint64_t *)c->part, static_cast<uint8_t *>(d_out), (uint64_t)cap,
-                            hdr, (uint64_t)nb, (uint32_t)(n - (nb - 1) * kBlk), c->boff);
-      continue;
-    }
     hipExtLaunchKernelGGL(lz4_emit, dim3((unsigned)(8 * ((ng * kGSplit + 7) / 8))), dim3(64 * kEW), 0, s, nullptr,
                           k + 1 == nchunks ? ev(ts ? ts->c : nullptr) : nullptr, 0u, in,
                           (const uint8_t *)c->slots, (const uint8_t *)ovfs, b0,
@@ -1876,8 +1665,6 @@ int lz4r_ctx_create(lz4r_ctx **out) {
   lz4r_ctx *c = new (std::nothrow) lz4r_ctx();
   if (!c) return LZ4R_ERR_NOMEM;
   if (hipGetDevice(&c->device) != hipSuccess ||
-      hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device) !=
-          hipSuccess ||
       hipMalloc(&c->len, 3 * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->len, 0, 3 * sizeof(uint64_t)) != hipSuccess) {
     lz4r_ctx_destroy(c);
