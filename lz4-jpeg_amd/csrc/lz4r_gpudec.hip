@@ -57,10 +57,6 @@
 
 namespace {
 
-// the sequence-parallel lz4_decode_seq instead of lz4_decode_blocks (tools A/B)
-#ifndef LZ4R_DEC_SEQ
-#define LZ4R_DEC_SEQ 0
-#endif
 constexpr int kBlk = LZ4R_BLOCK;
 constexpr int kInMax = LZ4R_BLOCK_BOUND;   // bytes of one encoded block (bound)
 constexpr int kLanes = 64;                 // threads per workgroup (one wave)
@@ -592,383 +588,6 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
   }
 }
 
-// ---- lz4_decode_seq: the sequence-parallel block decoder ---------------------
-// lz4_decode_blocks decodes a block per lane: each sequence's header is an
-// L2 round trip on the lane's chain (the next window's address is the size
-// field just read), half the wave's lanes idle, and the wave runs the longest
-// of its 32 blocks.  Here a wave takes 4 consecutive blocks (~62 sequences):
-//   1. stage  the blocks' bytes (contiguous: the compressor's offsets) in LDS
-//             with 16-B loads;
-//   2. hop    lane g walks block g's u16 size fields (one LDS round trip per
-//             sequence) and lists the sequence starts -- in the plain reading a
-//             sequence's size field is its length (LZ4.c:546-575; a truncated
-//             match over-counts by one, and such a block fails the checks below);
-//   3. parse  every sequence at once, lane = sequence: the plain reading of
-//             decode_block_plain (token nibbles, literal extension, distance,
-//             match extension), a wave scan of L + M for the output positions,
-//             and every consistency check of the plain path (a block that
-//             passes decodes to the bytes the general path returns);
-//   4. copy   literal runs flattened over the lanes as aligned 16-B words
-//             OR-ed into a zeroed LDS image (lz4_emit's literal pass, in
-//             reverse), then the matches in rounds: a match whose source bytes
-//             are all final (a per-byte ready bitmap) copies itself, in 16-B
-//             steps of a doubling distance (copy_match), and marks its bytes;
-//   5. store  the 1200 contiguous bytes as 16-B stores.
-// Anything else -- offsets that are not contiguous, a block over the stage, a
-// failed check, a dependency chain past kSRounds -- decodes the wave's blocks
-// with decode_block, a lane per block, exactly as lz4_decode_blocks' general
-// path (bit-identical results either way).
-constexpr int kSG = 4;                      // blocks per wave
-constexpr int kSPad = 16;                   // stage offset: literal words read up to 15 B before a run
-constexpr int kSStage = 2048;               // staged bytes per wave (text: ~1,240)
-constexpr int kSMaxSeq = 80;                // sequences per block on this path
-constexpr int kSRounds = 24;                // match dependency rounds before the fallback
-constexpr int kSOut = kSG * kBlk;           // 1200
-struct SeqLds {
-  alignas(16) uint8_t enc[kSPad + kSStage + 32];
-  alignas(16) uint8_t out[kSOut + 32];      // + slack: decode_block's reads past slot 3
-  uint16_t seq[kSG * kSMaxSeq + 2];
-  uint32_t rdy[kSOut / 32 + 2];             // byte x of out is final: bit x
-  uint32_t marks[64];
-  uint4 pmask[17];                          // pmask[k]: the low k bytes of 16 set
-};
-
-template <int CTRL, int ROW, int BANK>
-__device__ __forceinline__ uint32_t sdpp(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW, BANK, false);
-}
-__device__ __forceinline__ uint32_t s_incl_add(uint32_t v) {
-  v += sdpp<0x111, 0xf, 0xf>(v);
-  v += sdpp<0x112, 0xf, 0xf>(v);
-  v += sdpp<0x114, 0xf, 0xf>(v);
-  v += sdpp<0x118, 0xf, 0xf>(v);
-  v += sdpp<0x142, 0xa, 0xf>(v);
-  v += sdpp<0x143, 0xc, 0xf>(v);
-  return v;
-}
-__device__ __forceinline__ uint32_t s_incl_max(uint32_t v) {
-  v = max(v, sdpp<0x111, 0xf, 0xf>(v));
-  v = max(v, sdpp<0x112, 0xf, 0xf>(v));
-  v = max(v, sdpp<0x114, 0xf, 0xf>(v));
-  v = max(v, sdpp<0x118, 0xf, 0xf>(v));
-  v = max(v, sdpp<0x142, 0xa, 0xf>(v));
-  v = max(v, sdpp<0x143, 0xc, 0xf>(v));
-  return v;
-}
-__device__ __forceinline__ uint32_t s_lane63(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-__device__ __forceinline__ void s_sync() {          // a wave's LDS operations are served in order
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-}
-// bytes x .. x + 3 of an LDS byte array (x >= 0), from two aligned dwords
-__device__ __forceinline__ uint32_t lds_ld4(const uint8_t *b, int x) {
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(b + (x & ~3));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)x & 3u);
-}
-// bits [lo, hi) of a dword, 0 <= lo <= hi <= 32
-__device__ __forceinline__ uint32_t bit_range(int lo, int hi) {
-  const uint32_t h = hi >= 32 ? ~0u : (1u << hi) - 1u;
-  return h & ~((1u << lo) - 1u);
-}
-// bytes [lo, hi) of a dword (clamped to 0..4), as a bit mask
-__device__ __forceinline__ uint32_t byte_range(int lo, int hi) {
-  lo = min(max(lo, 0), 4);
-  hi = min(max(hi, lo), 4);
-  return bit_range(8 * lo, 8 * hi);
-}
-// OR the first n (1..16) bytes of v into the zero bytes at b[a .. a + n)
-__device__ __forceinline__ void lds_or16(uint8_t *b, int a, const uint32_t (&v)[4], int n) {
-  const int sh = a & 3;
-  uint32_t *w = reinterpret_cast<uint32_t *>(b + (a & ~3));
-  uint32_t u[5];
-  if (sh == 0) {
-    u[0] = v[0]; u[1] = v[1]; u[2] = v[2]; u[3] = v[3]; u[4] = 0u;
-  } else {
-    const uint32_t c = (uint32_t)(4 - sh);
-    u[0] = __builtin_amdgcn_alignbyte(v[0], 0u, c);
-    u[1] = __builtin_amdgcn_alignbyte(v[1], v[0], c);
-    u[2] = __builtin_amdgcn_alignbyte(v[2], v[1], c);
-    u[3] = __builtin_amdgcn_alignbyte(v[3], v[2], c);
-    u[4] = __builtin_amdgcn_alignbyte(0u, v[3], c);
-  }
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const uint32_t m = byte_range(sh - 4 * k, sh + n - 4 * k);
-    if (m) atomicOr(&w[k], u[k] & m);
-  }
-}
-// 16 bytes of an LDS byte array at x >= 0
-__device__ __forceinline__ void lds_ld16(const uint8_t *b, int x, uint32_t (&v)[4]) {
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(b + (x & ~3));
-  const uint32_t sh = (uint32_t)x & 3u;
-  const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
-  v[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
-  v[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
-  v[2] = __builtin_amdgcn_alignbyte(d3, d2, sh);
-  v[3] = __builtin_amdgcn_alignbyte(d4, d3, sh);
-}
-// mark out bytes [a, a + n) final
-__device__ __forceinline__ void rdy_set(uint32_t *rdy, int a, int n) {
-  for (int x = a; x < a + n; x = (x | 31) + 1)
-    atomicOr(&rdy[x >> 5], bit_range(x & 31, min(a + n - (x & ~31), 32)));
-}
-__device__ __forceinline__ bool rdy_all(const uint32_t *rdy, int a, int n) {
-  bool ok = true;
-  for (int x = a; x < a + n; x = (x | 31) + 1) {
-    const uint32_t m = bit_range(x & 31, min(a + n - (x & ~31), 32));
-    ok = ok && (rdy[x >> 5] & m) == m;
-  }
-  return ok;
-}
-
-__global__ __launch_bounds__(kLanes) void lz4_decode_seq(
-    const uint8_t *__restrict__ in, size_t in_len, const uint64_t *__restrict__ boff,
-    size_t nb, uint8_t *__restrict__ out, size_t out_cap,
-    unsigned long long *__restrict__ result, const unsigned long long *__restrict__ nb_dev,
-    const unsigned long long *__restrict__ gate) {
-  __shared__ SeqLds S;
-  const int lane = threadIdx.x;
-  const size_t b0 = (size_t)blockIdx.x * kSG;
-  if (nb_dev) {
-    if (*gate != 0) return;
-    nb = (size_t)*nb_dev;
-  }
-  if (b0 >= nb) return;
-  const int nl = (int)(nb - b0 < (size_t)kSG ? nb - b0 : kSG);
-  // block g = [beg_g, end_g) of the stream; end of the last = the next offset or in_len
-  size_t bv = 0;
-  if (lane <= nl) bv = lane < nl || b0 + (size_t)nl < nb ? 1 + boff[b0 + lane] : in_len;
-  size_t beg[kSG + 1];
-#pragma unroll
-  for (int g = 0; g <= kSG; ++g)
-    beg[g] = (size_t)__builtin_amdgcn_readlane((int)(uint32_t)bv, g) |
-             (size_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bv >> 32), g) << 32;
-  const size_t A = beg[0] & ~(size_t)15, E = beg[nl];
-  bool fast = E <= in_len && E >= A && E - A <= (size_t)kSStage;
-#pragma unroll
-  for (int g = 0; g < kSG; ++g)
-    if (g < nl) fast = fast && beg[g + 1] >= beg[g] + 3 && beg[g + 1] - beg[g] <= (size_t)kInMax;
-  int qlast = 0;                                    // decoded bytes of block nl - 1
-  uint32_t okm = 0;                                 // (fallback) blocks decoded, a bit each
-  if (fast) {
-    // ---- 1. stage: stream byte A + x at S.enc[kSPad + x] --------------------------
-    const int nbytes = (int)(E - A), nch = (nbytes + 15) >> 4;
-    for (int c = lane; c < nch; c += kLanes) {
-      const size_t a = A + 16 * (size_t)c;
-      uint4 v;
-      if (a + 16 <= in_len) {
-        v = *reinterpret_cast<const uint4 *>(in + a);
-      } else {
-        uint8_t t[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) t[j] = a + j < in_len ? in[a + j] : 0;
-        v = *reinterpret_cast<const uint4 *>(t);
-      }
-      *reinterpret_cast<uint4 *>(&S.enc[kSPad + 16 * c]) = v;
-    }
-    for (int i = lane; i < (kSOut + 32) / 16; i += kLanes)
-      reinterpret_cast<uint4 *>(S.out)[i] = make_uint4(0, 0, 0, 0);
-    if (lane < kSOut / 32 + 2) S.rdy[lane] = 0u;
-    if (lane < 17) {
-      uint32_t m[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) m[j] = byte_range(0, lane - 4 * j);
-      S.pmask[lane] = make_uint4(m[0], m[1], m[2], m[3]);
-    }
-    s_sync();
-    // ---- 2. headers and the hop -------------------------------------------------
-    const int og = lane < nl ? (int)(beg[lane] - A) + kSPad : 0;
-    const int eg = lane < nl ? (int)(beg[lane + 1] - A) + kSPad : 0;
-    const uint32_t h = lane < nl ? lds_ld4(S.enc, og) : 0u;
-    const int nseq = (int)(h & 255u), want = (int)((h >> 8) & 0xFFFFu) - 3;
-    bool good = lane >= nl || (nseq >= 1 && nseq <= kSMaxSeq && want == eg - og - 3);
-    const uint32_t sinc = s_incl_add(lane < nl ? (uint32_t)nseq : 0u);
-    const int sb = (int)sinc - nseq;                  // flat index of the block's first sequence
-    const int Stot = (int)s_lane63(sinc);
-    if (lane < nl && good) {
-      int ip = og + 3;
-      for (int k = 0; k < nseq; ++k) {
-        S.seq[sb + k] = (uint16_t)ip;
-        const int Sz = (int)((lds_ld4(S.enc, ip) >> 8) & 0xFFFFu);
-        if (Sz < 5 || ip + Sz > eg) {
-          good = false;
-          break;
-        }
-        ip += Sz;
-      }
-      good = good && ip == eg;
-    }
-    fast = __builtin_amdgcn_ballot_w64(!good) == 0;
-    s_sync();
-    // per block (SGPRs): first flat sequence, count, byte range
-    int sbg[kSG + 1], nsg[kSG], egs[kSG];
-#pragma unroll
-    for (int g = 0; g < kSG; ++g) {
-      sbg[g] = g < nl ? __builtin_amdgcn_readlane(sb, g) : Stot;
-      nsg[g] = g < nl ? __builtin_amdgcn_readlane(nseq, g) : 0;
-      egs[g] = g < nl ? __builtin_amdgcn_readlane(eg, g) : 0;
-    }
-    sbg[kSG] = Stot;
-    const bool last_in_stream = b0 + (size_t)nl == nb;
-    // ---- 3-4. rounds of 64 sequences: parse, literals, matches -------------------
-    uint32_t carry = 0;                               // output bytes of the earlier rounds
-    for (int f0 = 0; fast && f0 < Stot; f0 += kLanes) {
-      const int f = f0 + lane;
-      const bool valid = f < Stot;
-      int g = 0;
-#pragma unroll
-      for (int j = 1; j < kSG; ++j) g += f >= sbg[j] ? 1 : 0;
-      int sbf = sbg[0], nsf = nsg[0], egf = egs[0];
-#pragma unroll
-      for (int j = 1; j < kSG; ++j)
-        if (g == j) { sbf = sbg[j]; nsf = nsg[j]; egf = egs[j]; }
-      const int k = f - sbf;
-      const bool lastseq = k == nsf - 1;
-      const int ip = valid ? (int)S.seq[f] : kSPad;
-      // the plain reading (decode_block_plain): bytes ip .. ip + 7
-      const uint32_t *wp = reinterpret_cast<const uint32_t *>(S.enc + (ip & ~3));
-      const uint32_t sh = (uint32_t)ip & 3u;
-      const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2];
-      const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-      const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-      const int tok = (int)(w0 & 255), Sz = (int)((w0 >> 8) & 0xFFFF);
-      const int e0 = (int)(w0 >> 24), e1 = (int)(w1 & 255);
-      const int tl = tok >> 4, tm = tok & 15;
-      const int mx = tm == 15 ? 1 : 0;
-      const bool big = tl == 15;
-      const bool ff = e0 == 255;
-      const int le = (big ? 1 : 0) + ((big & ff) ? 1 : 0);
-      const int Lb = Sz - 5 - le - mx;
-      const int L = big ? Lb : tl;
-      const int r = (L - 15) & 255;
-      const bool okb = (L >= 15) & ((ff & (r == 255) & (e1 == 0)) | (!ff & (r == e0)));
-      const bool oks = Sz == L + 5 + mx;
-      bool ok = valid && ((big & okb) | (!big & oks)) && L >= 0;
-      const int lit = ip + 3 + le;
-      const uint32_t t = ok ? lds_ld4(S.enc, lit + L) : 0u;   // distance bytes, match extension
-      const int D = (int)(t & 0xFFFF);
-      const bool hasm = D != 0;
-      const int M = hasm ? (mx ? 19 + (int)((t >> 16) & 255) : tm + 4) : 0;
-      ok = ok && (hasm || (lastseq && tm == 0)) && lit + L + 2 + mx <= egf;
-      const uint32_t x = ok ? (uint32_t)(L + M) : 0u;
-      const uint32_t incl = s_incl_add(x) + carry;
-      carry = s_lane63(incl);
-      const int pos = (int)(incl - x);                // this sequence's first output byte
-      const int prel = pos - kBlk * g;                // ... within its block
-      ok = ok && prel + L <= kBlk && (!hasm || (D <= prel + L && prel + L + M <= kBlk));
-      if (ok && lastseq) {
-        const int endb = prel + L + M;
-        ok = (last_in_stream && g == nl - 1) ? endb >= 1 : endb == kBlk;
-        if (g == nl - 1) qlast = endb;
-      }
-      fast = __builtin_amdgcn_ballot_w64(valid && !ok) == 0;
-      if (!fast) break;
-      qlast = (int)__builtin_amdgcn_readlane(qlast, 63 - __builtin_clzll(
-          __builtin_amdgcn_ballot_w64(valid && lastseq && g == nl - 1) | 1ull));
-      // ---- literals: aligned 16-B words of out, OR-ed from the staged bytes ----
-      {
-        const int ob = pos;
-        const int cw = ok && L > 0 ? ((ob + L - 1) >> 4) - (ob >> 4) + 1 : 0;
-        const uint32_t cinc = s_incl_add((uint32_t)cw);
-        const int C = (int)s_lane63(cinc);
-        const int stw = (int)sdpp<0x138, 0xf, 0xf>(cinc);   // wave_shr:1: exclusive
-        const uint32_t rw = ((uint32_t)((ob >> 4) - stw) & 0xFFFFu) | ((uint32_t)(lit - ob) << 16);
-        const uint32_t rb = (uint32_t)ob | ((uint32_t)(ob + L) << 16);
-        uint32_t cr = 0;
-        for (int w0i = 0; w0i < C; w0i += kLanes) {
-          s_sync();
-          S.marks[lane] = 0u;
-          if (cw > 0 && stw >= w0i && stw < w0i + kLanes) S.marks[stw - w0i] = (uint32_t)lane + 1u;
-          s_sync();
-          const uint32_t k1 = max(s_incl_max(S.marks[lane]), cr);
-          cr = s_lane63(k1);
-          const int gw = w0i + lane;
-          const int kr = ((int)k1 - 1) & 63;
-          const uint32_t kw = (uint32_t)__shfl((int)rw, kr, 64);
-          const uint32_t kb = (uint32_t)__shfl((int)rb, kr, 64);
-          if (gw < C) {
-            const int tw = 16 * ((int)(int16_t)(kw & 0xFFFFu) + gw);   // the word's first out byte
-            const int xs = tw + ((int)kw >> 16);                        // its staged bytes
-            const uint32_t *iw = reinterpret_cast<const uint32_t *>(S.enc + (xs & ~3));
-            const uint32_t a0 = iw[0], a1 = iw[1], a2 = iw[2], a3 = iw[3], a4 = iw[4];
-            const uint32_t ssh = (uint32_t)xs & 3u;
-            const int lb = max((int)(kb & 0xFFFFu) - tw, 0), hb = min((int)(kb >> 16) - tw, 16);
-            const uint4 ml = S.pmask[lb], mh = S.pmask[hb];
-            const uint32_t v0 = __builtin_amdgcn_alignbyte(a1, a0, ssh) & (ml.x ^ mh.x);
-            const uint32_t v1 = __builtin_amdgcn_alignbyte(a2, a1, ssh) & (ml.y ^ mh.y);
-            const uint32_t v2 = __builtin_amdgcn_alignbyte(a3, a2, ssh) & (ml.z ^ mh.z);
-            const uint32_t v3 = __builtin_amdgcn_alignbyte(a4, a3, ssh) & (ml.w ^ mh.w);
-            atomicOr(reinterpret_cast<unsigned long long *>(S.out + tw), (unsigned long long)v1 << 32 | v0);
-            atomicOr(reinterpret_cast<unsigned long long *>(S.out + tw + 8), (unsigned long long)v3 << 32 | v2);
-            atomicOr(&S.rdy[tw >> 5], (((1u << hb) - 1u) ^ ((1u << lb) - 1u)) << (tw & 16));
-          }
-        }
-      }
-      s_sync();
-      // ---- matches, in dependency rounds -----------------------------------------
-      {
-        const int q = pos + L;
-        bool pend = ok && M > 0;
-        for (int it = 0; __builtin_amdgcn_ballot_w64(pend) != 0; ++it) {
-          if (it == kSRounds) {
-            fast = false;
-            break;
-          }
-          const bool go = pend && rdy_all(S.rdy, q - D, min(D, M));
-          s_sync();
-          if (go) {
-            int i = 0, d = D;
-            while (i < M) {
-              int n = min(M - i, 16);
-              n = min(n, d);
-              uint32_t v[4];
-              lds_ld16(S.out, q + i - d, v);
-              lds_or16(S.out, q + i, v, n);
-              i += n;
-              if (d < 16) d = i + D;
-            }
-            rdy_set(S.rdy, q, M);
-            pend = false;
-          }
-          s_sync();
-        }
-      }
-    }
-  }
-  // ---- fallback: the general decoder, a lane per block -----------------------------
-  if (!fast) {
-    int q = 0;
-    if (lane < nl) {
-      const size_t bg = beg[lane], en = beg[lane + 1];
-      const bool last = b0 + (size_t)lane == nb - 1;
-      if (en >= bg + 3 && en <= in_len && en - bg <= (size_t)kInMax)
-        q = decode_block(Bytes<true>{in + bg, in_len - bg}, (int)(en - bg), last,
-                         Slot{S.out + lane * kBlk});
-      if (q == 0) atomicMin(&result[1], (unsigned long long)(b0 + lane) + 1);
-    }
-    qlast = __builtin_amdgcn_readlane(q, nl - 1);
-    s_sync();
-  }
-  if (b0 + (size_t)nl == nb && lane == 0) result[0] = (unsigned long long)((nb - 1) * kBlk + qlast);
-  // ---- 5. store: out bytes [300 b0, 300 b0 + total) --------------------------------
-  size_t total = (size_t)kBlk * (nl - 1) + (size_t)(qlast > 0 ? qlast : 0);
-  const size_t o0 = b0 * (size_t)kBlk;
-  if (o0 >= out_cap) return;
-  if (o0 + total > out_cap) total = out_cap - o0;
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  if (((reinterpret_cast<uintptr_t>(out) + o0) & 15) == 0) {
-    const int nv = (int)(total >> 4);
-    for (int v = lane; v < nv; v += kLanes)
-      __builtin_nontemporal_store(reinterpret_cast<const u32x4 *>(S.out)[v],
-                                  reinterpret_cast<u32x4 *>(out + o0) + v);
-    for (size_t i = (size_t)nv * 16 + lane; i < total; i += kLanes) out[o0 + i] = S.out[i];
-  } else {
-    for (size_t i = lane; i < total; i += kLanes) out[o0 + i] = S.out[i];
-  }
-}
-
 // ---- bare streams: block boundaries found on the device ---------------------
 // LZ4_decode (LZ4.c:1038) takes only the file.  The stream is cut into
 // chunks of kChunkB bytes; in each chunk the first position that parses as
@@ -1360,14 +979,6 @@ extern "C" int lz4r_decompress_device(const void *d_in, size_t in_len, const voi
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(lz4_decode_init, dim3(1), dim3(1), 0, s,
                      static_cast<unsigned long long *>(d_result));
-  if (LZ4R_DEC_SEQ) {
-    hipLaunchKernelGGL(lz4_decode_seq, dim3((unsigned)((nb + kSG - 1) / kSG)), dim3(kLanes), 0, s,
-                       static_cast<const uint8_t *>(d_in), in_len,
-                       static_cast<const uint64_t *>(d_block_offsets), nb,
-                       static_cast<uint8_t *>(d_out), out_cap,
-                       static_cast<unsigned long long *>(d_result), nullptr, nullptr);
-    return hipGetLastError() == hipSuccess ? LZ4R_OK : LZ4R_ERR_HIP;
-  }
   const unsigned grid = (unsigned)((nb + kBPW - 1) / kBPW);
   hipLaunchKernelGGL(lz4_decode_blocks, dim3(grid), dim3(kLanes), 0, s,
                      static_cast<const uint8_t *>(d_in), in_len,
@@ -1419,14 +1030,9 @@ int bare_pass(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap, si
   hipLaunchKernelGGL(lz4_bare_offsets<kExact>, dim3(ng), dim3(64), 0, s, in, in_len, nchunks, cand,
                      cnt, gbase, boff, (uint64_t)nb_cap, lists, lok);
   hipLaunchKernelGGL(lz4_bare_gate, dim3(1), dim3(1), 0, s, in, small, (uint64_t)nb_cap);
-  if (LZ4R_DEC_SEQ)
-    hipLaunchKernelGGL(lz4_decode_seq, dim3((unsigned)((nb_cap + kSG - 1) / kSG)), dim3(kLanes), 0,
-                       s, in, in_len, static_cast<const uint64_t *>(boff), nb_cap, out, out_cap,
-                       d_res, d_nb, d_gate);
-  else
-    hipLaunchKernelGGL(lz4_decode_blocks, dim3((unsigned)((nb_cap + kBPW - 1) / kBPW)),
-                       dim3(kLanes), 0, s, in, in_len, static_cast<const uint64_t *>(boff), nb_cap,
-                       out, out_cap, d_res, d_nb, d_gate);
+  hipLaunchKernelGGL(lz4_decode_blocks, dim3((unsigned)((nb_cap + kBPW - 1) / kBPW)),
+                     dim3(kLanes), 0, s, in, in_len, static_cast<const uint64_t *>(boff), nb_cap,
+                     out, out_cap, d_res, d_nb, d_gate);
   if (own) (void)hipFreeAsync(own, s);
   unsigned long long h[5] = {0, 0, 0, 0, 0};          // nb, status, result[2], gate
   if (hipMemcpyAsync(h, small, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
