@@ -62,7 +62,7 @@ def log(*a):
 def _profile_json(path):
     """This round's profile, else the latest earlier round's."""
     base = os.path.basename(path)[:4]
-    for r in ("r05_", "r04_", "r03_", "r02_", "r01_"):
+    for r in ("r06_", "r05_", "r04_", "r03_", "r02_", "r01_"):
         p = path.replace(base, r)
         if os.path.exists(p):
             return p
