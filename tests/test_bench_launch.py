@@ -93,3 +93,28 @@ def test_workload_shares_cover(world):
 
 def test_cpu_cores_positive():
     assert bench.host_cpu_cores() >= 1
+
+
+def test_phase_watchdog_ends_a_stuck_rank():
+    """bench.phase(): a rank whose phase outlives its limit (a collective that
+    never completes on the first 8-GPU run) dumps every thread's stack and
+    exits non-zero with the phase named, instead of sitting until the
+    driver's limit kills the run silently."""
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "bench.phase('lz4 gather', 3, 2); time.sleep(60)" % REPO)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=50)
+    assert r.returncode != 0
+    assert "rank 3: phase lz4 gather" in r.stderr
+    assert "Timeout" in r.stderr and "time.sleep" not in r.stdout     # faulthandler's dump
+
+
+def test_phase_watchdog_is_rearmed_per_phase():
+    """Each phase() call replaces the previous deadline: a run whose phases
+    each finish in time is not killed however long the whole run takes."""
+    code = ("import faulthandler, sys, time; sys.path.insert(0, %r); import bench\n"
+            "for k in range(4):\n"
+            "    bench.phase('p%%d' %% k, 0, 2); time.sleep(1)\n"
+            "faulthandler.cancel_dump_traceback_later(); print('done')" % REPO)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=50)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip() == "done"
