@@ -117,3 +117,10 @@ def test_bench_distributed_path_at_world1(gpu):
     assert line["lz4_gather_ok"] is True and line["value"] > 0
     assert line["lz4_decode"]["roundtrip_ok"] is True
     assert line["jpeg"]["value"] > 0
+    # the fail-fast additions: per-rank times, the gather's piece size, the
+    # phases each rank announces (its watchdog is armed per phase)
+    pr = line["per_rank"]
+    assert len(pr["call_ms"]) == 1 and pr["call_ms"][0] > 0 and len(pr["step_ms"]) == 1
+    assert line["lz4_gather_chunk_bytes"] == 1 << 30
+    for ph in ("init_process_group", "lz4 warm-up", "lz4 timed steps", "lz4 gather", "jpeg"):
+        assert f"rank 0: phase {ph}" in res.stderr, ph
