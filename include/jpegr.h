@@ -115,12 +115,13 @@ const char *jpegr_strerror(int code);
  *            code length << 16, in the reference's codes[] (DFS) order;
  *            the codes follow from the lengths: code[0] = 0, code[k] =
  *            (code[k-1] + 1) shifted left (or right) to length len[k]
- * d_coef 16-B aligned; d_bits 4-B aligned to encode, 16-B aligned to decode
- * (JPEGR_ERR_ARG otherwise).
+ * d_coef 16-B aligned; d_bits 4-B aligned to encode, d_bits and d_table
+ * 16-B aligned to decode (JPEGR_ERR_ARG otherwise).
  * d_scratch: jpegr_entropy_scratch_bytes(ntiles) device bytes.  d_status:
- * 2 u32 on the device; [0] = streams whose code or sequence would overflow
- * the reference's char code[32] / sequence[1024|512] buffers (undefined
- * behaviour there; truncated here).  Asynchronous on `stream`. */
+ * 3 u32 on the device, shared by both calls; [0] = streams whose code or
+ * sequence would overflow the reference's char code[32] / sequence[1024|512]
+ * buffers (undefined behaviour there; truncated here).  Asynchronous on
+ * `stream`. */
 size_t jpegr_entropy_scratch_bytes(size_t ntiles);
 int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, void *d_bits,
                                 void *d_meta, void *d_table, void *d_scratch,
@@ -130,7 +131,10 @@ int jpegr_entropy_encode_device(const void *d_coef, size_t ntiles, void *d_bits,
  * stream has an empty sequence and stands for rle_len copies of its symbol,
  * which the reference keeps in its RLE array) -> ints (inverse_RLE, :810:
  * counts clamped to the stream length, zero fill), written in
- * jpegr_encode_device's layout.  d_status[1] = malformed streams. */
+ * jpegr_encode_device's layout.  d_status[1] = malformed streams, set by
+ * the call itself (no memset needed); d_status[2] is the call's tag, which
+ * orders the kernel's own zeroing of [1] before any count is added (keep it
+ * to the library; one decode at a time per status array). */
 int jpegr_entropy_decode_device(const void *d_bits, const void *d_meta,
                                 const void *d_table, size_t ntiles, void *d_coef,
                                 void *d_status, void *stream);

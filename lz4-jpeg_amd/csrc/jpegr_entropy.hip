@@ -37,7 +37,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <mutex>
+#include <atomic>
 #include <type_traits>
 
 #include "../../include/jpegr.h"
@@ -883,16 +883,31 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
 // left-aligned codes in registers, each code's value and length in LDS as one
 // u16 (value in 11 bits, two's complement, | length << 11: every value of a
 // 4K image's streams fits; a stream whose values or lengths do not takes the
-// slow path), in a dword-column layout (two codes per dword of the lane's own
-// bank).  11.5 / 5.9 KB per wave with the decoded ints: a 4K image's 2,025
-// luma waves and 2,025 chroma waves (a lane decodes the tile's Cr, then its
-// Cb stream) are all resident at once, the two kernels side by side.
+// slow path), one row of u16 per code.  With the decoded ints and the luma
+// start map: 13.6 KB per luma wave, 5.9 KB per chroma wave (a lane decodes
+// the tile's Cr, then its Cb stream), one of each per workgroup: a 4K image's
+// 2,025 workgroups are all resident at once.
 template <int N, int Cap>
 struct DecLds {
-  uint32_t vl[Cap / 2][kLanes];            // codes 2i, 2i + 1: value | len << 11 (u16 each)
+  uint16_t vl[Cap][kLanes];                // code k: value | len << 11 (row k, the lane's u16)
   // the lane's decoded ints; rows of N + 2 (an odd number of dwords), so the
   // lanes' stores at one index hit 64 different banks (rows of N: 32-way)
   alignas(16) int16_t out[kLanes][N + 2];
+  // luma: the lane's code starts as a 256-bit map over the 8-bit windows
+  // (row r, bit 31 - i: window 32 r + i), for streams whose codes are all
+  // <= 8 bits long
+  uint32_t bm[N == 64 ? 8 : 1][kLanes];
+};
+
+// One lane's u16 column of a [rows][64] u16 block: entry k at byte k * 128
+// (one address op per lookup; two lanes share a dword, so lanes reading
+// different rows of the same bank pair conflict two-way at most)
+struct VRow {
+  typedef uint16_t __attribute__((may_alias)) HA;
+  uint8_t *p;                                   // &block[0][lane] as bytes
+  __device__ __forceinline__ HA &operator[](int k) const {
+    return *reinterpret_cast<HA *>(p + (uint32_t)k * (2 * kLanes));
+  }
 };
 
 // The number of k < Cap with h[k] > w (31-bit values): the borrows of
@@ -901,7 +916,7 @@ struct DecLds {
 // at least eight instructions after its write: no hazard wait states; a
 // group of four pads with an s_nop).
 template <int Cap>
-__device__ __forceinline__ int count_above(uint32_t w, const uint32_t (&h)[Cap]) {
+__device__ __forceinline__ uint32_t count_above(uint32_t w, const uint32_t (&h)[Cap]) {
   static_assert(Cap % 4 == 0, "groups of four");
   uint32_t a = 0, b = 0;
   if constexpr (Cap % 8 == 4) {
@@ -950,112 +965,201 @@ __device__ __forceinline__ int count_above(uint32_t w, const uint32_t (&h)[Cap])
           [h3] "v"(h[g + 3]), [h4] "v"(h[g + 4]), [h5] "v"(h[g + 5]), [h6] "v"(h[g + 6]),
           [h7] "v"(h[g + 7]));
   }
-  return (int)(a + b);
+  return a + b;
 }
 
 // Decode one stream: bits + table -> RLE ints (decode_huffman) -> n ints
 // (inverse_RLE: counts clamped to n, zero fill).  With one code (empty bit
 // string) the reference decodes nothing and keeps its RLE ints: rle_len
-// copies of the symbol.  Returns false on a malformed stream.
-// The left-aligned codes of a stream with at most Cap codes live in
-// registers (lc[k] for k < U, all ones past U): the symbol at a window is the
-// count of codes <= the window, minus one -- Cap independent compares
-// instead of a binary search whose every step waited on an LDS read.  Only
-// the matched entry's value | length is read from LDS (vl).
+// copies of the symbol.  tb: the table's first Cap entries; q0, q1: the
+// first two 16-B chunks of the bits (loaded by the caller with the meta
+// word); bm: the lane's start-map column (luma) or null.
+// The symbol at a window is the count of codes <= it, minus one: the codes
+// of a table built from a tree increase strictly (DFS order; a table whose
+// codes do not is no tree and takes the slow path, which matches codes in
+// table order).  When every code of the wave is <= 8 bits (a random 4K
+// image's luma) the count is one row of a 256-bit map of the code starts
+// plus that row's prefix count; otherwise Cap compares against the
+// left-aligned codes in registers.  Only the matched entry's value | length
+// is read from LDS (vl).
+// The walk goes a (count, value) pair per step, so the inverse RLE's fill runs
+// once per pair with every lane of the wave on it, and no lane carries a
+// count across steps; the bit buffer is refilled once per one, two or four
+// symbols, as the wave's longest code allows.  Every instruction of the walk
+// counts: a wave issues at most one per four cycles, and two luma and two
+// chroma waves share each SIMD.
 // Returns 1 (decoded), 0 (malformed) or -1 (a value or length that the u16
-// entries cannot hold: the caller runs decode_stream_slow).
+// entries cannot hold, or codes that do not increase: the caller runs
+// decode_stream_slow).
 template <int Cap, typename VlT>
 __device__ int decode_stream(const uint8_t *__restrict__ bits, uint32_t m,
-                             const uint32_t *__restrict__ table, VlT vl,
-                             int16_t *__restrict__ out, int n) {
+                             const uint32_t (&tb)[Cap], uint4 q0, uint4 q1, VlT vl,
+                             int16_t *__restrict__ out, int n, uint32_t *bm) {
   const int nbits = (int)(m & 0xFFFF), R = (int)((m >> 16) & 255), U = (int)(m >> 24);
   if (U == 0 || U > Cap || R == 0 || R > 2 * n) return 0;
-  // codes from the lengths, left to right (DFS order)
-  uint32_t lc[Cap];
-  uint32_t code = 0;
-  int plen = 0;
+  // codes from the lengths, left to right (DFS order); lh[k] = lc[k] >> 1 (a
+  // code of <= 31 bits leaves bit 0 of its left-aligned form clear), all ones
+  // past U: above every 31-bit window, never counted as <= it
+  uint32_t lh[Cap];
+  uint32_t code = 0, prev = 0;
+  int plen = 0, lmax = 0;
   bool bad = false, wide = false;
 #pragma unroll
   for (int k = 0; k < Cap; ++k) {
-    lc[k] = ~0u;
+    lh[k] = ~0u;
     if (k < U) {
-      const uint32_t e = table[k];
+      const uint32_t e = tb[k];
       const int L = (int)((e >> 16) & 255);
       const int v = (int16_t)(e & 0xFFFF);
       bad = bad || L > 32 || (U > 1 && L == 0);
       wide = wide || L > 31 || v < -1024 || v > 1023;
       if (k) code = L >= plen ? (code + 1) << (L - plen) : (code + 1) >> (plen - L);
       plen = L;
-      lc[k] = L ? code << (32 - L) : 0;
+      lmax = max(lmax, L);
+      const uint32_t lc = L ? code << (32 - L) : 0;
+      wide = wide || (k && lc <= prev);
+      prev = lc;
+      lh[k] = lc >> 1;
       vl[k] = (uint16_t)(((uint32_t)v & 0x7FFu) | ((uint32_t)L << 11));
     }
   }
   if (bad) return 0;
   if (wide) return -1;
-  int idx = 0, pending = -1;                        // pending: a count awaiting its value
-  auto put = [&](int v) {
-    if (pending < 0) {
-      pending = v;
-      return;
+  int idx = 0;
+  // a run of cnt copies of v at idx (clamped to the row): the first store
+  // unconditionally (past the run it is overwritten by the next run or the
+  // final zero fill; the row has spare slots), a loop only for longer runs
+  // (an empty asm keeps the loop a loop: as a memset it compiled to three
+  // nested loops whose exec-mask bookkeeping every pair paid)
+  auto fill = [&](int cnt, int v) {
+    const int c = min(cnt, n - idx);
+    out[idx] = (int16_t)v;
+    for (int j = 1; j < c; ++j) {
+      out[idx + j] = (int16_t)v;
+      asm volatile("");
     }
-    int cnt = pending;
-    pending = -1;
-    if (idx + cnt > n) cnt = n - idx;
-    for (int j = 0; j < cnt; ++j) out[idx++] = (int16_t)v;
+    idx += max(c, 0);
   };
   // an entry's value (11-bit two's complement) and length
   auto val = [](uint32_t e) { return (int)((int32_t)(e << 21) >> 21); };
   if (U == 1) {
     const int v = val(vl[0]);
-    for (int j = 0; j < R; ++j) put(v);
+    for (int j = 0; j + 1 < R; j += 2) fill(v, v);
   } else {
     // MSB-first bit buffer: acc holds nacc valid bits, left-aligned; words
-    // come from 16-B chunks of the stream's slot, the next chunk in flight
+    // come from 16-B chunks of the stream's slot, the next chunk in flight.
+    // Chunks past the bits are read too (they lie in the slot, and what they
+    // hold cannot change a decode: see lookup), so the load needs no select.
     const uint4 *src = reinterpret_cast<const uint4 *>(bits);
-    const int nch = (nbits + 127) >> 7;               // chunks holding the bits
-    uint4 q = src[0], nxt = nch > 1 ? src[1] : make_uint4(0, 0, 0, 0);
+    const int last = n / 8 - 1;                       // the slot's last chunk
+    uint4 q = q0, nxt = q1;
     int qi = 0, ci = 1;
     uint64_t acc = 0;
     int nacc = 0, p = 0, got = 0;
-    uint32_t lh[Cap];
+    // s codes lie above the window, a suffix of the increasing codes: the
+    // entry is k = Cap - 1 - s, at byte -128 s from entry Cap - 1
+    const uint8_t *vbase = reinterpret_cast<const uint8_t *>(&vl[Cap - 1]);
+    // Codes of at most 8 bits in every stream of the wave: the symbol at a
+    // window is found from its top 8 bits as the count of code starts <= them
+    // -- one row of the lane's 256-bit start map (LDS, built with ors) and
+    // that row's prefix count (registers, a byte each) instead of Cap
+    // compares.  Wave-uniform, so no lane walks both.
+    const bool narrow = __ballot(lmax > 8) == 0;      // every code <= 8 bits
+    const bool mid = __ballot(lmax > 16) == 0;        // every code <= 16 bits
+    const bool use_bm = bm != nullptr && narrow;
+    uint32_t pa = 0, pb = 0;
+    if (use_bm) {
 #pragma unroll
-    for (int k = 0; k < Cap; ++k) lh[k] = lc[k] >> 1;
-    while (p < nbits) {
+      for (int r = 0; r < 8; ++r) bm[r * kLanes] = 0u;
+#pragma unroll
+      for (int k = 0; k < Cap; ++k)
+        if (k < U) {
+          const uint32_t st = lh[k] >> 23;       // the code's top 8 bits
+          atomicOr(&bm[(st >> 5) * kLanes], 0x80000000u >> (st & 31));
+        }
+      uint32_t run = 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        if (r < 4) pa |= run << (8 * r);
+        else pb |= run << (8 * (r - 4));
+        run += __builtin_popcount(bm[r * kLanes]);
+      }
+    }
+    auto refill = [&]() {
       if (nacc <= 32) {                               // refill 32 bits (codes <= 31)
-        const uint32_t wd = qi == 0 ? q.x : qi == 1 ? q.y : qi == 2 ? q.z : q.w;
+        // the chunk's words move down as they are used (an indexed select
+        // became a scratch array)
+        const uint32_t wd = q.x;
+        q.x = q.y;
+        q.y = q.z;
+        q.z = q.w;
         acc |= (uint64_t)__builtin_bswap32(wd) << (32 - nacc);
         nacc += 32;
         if (++qi == 4) {
           qi = 0;
           q = nxt;
-          ++ci;
-          nxt = ci < nch ? src[ci] : make_uint4(0, 0, 0, 0);
+          ci = ci < last ? ci + 1 : ci;
+          nxt = src[ci];
         }
       }
-      // 32 bits at p (zero past the end)
-      uint32_t win = (uint32_t)(acc >> 32);
-      if (nbits - p < 32) win &= ~0u << (32 - (nbits - p));
-      // largest k with lc[k] <= win: the codes increase, so it is the count
-      // of codes <= win, minus one (lc[0] = 0; the all-ones entries past U
-      // count only for an all-ones window, whose code is the last).  Counted
-      // as Cap minus the borrows of win - lc[k] on 31 bits (a code of <= 31
-      // bits leaves bit 0 of its left-aligned form clear, so dropping it
-      // loses nothing), in two carry chains through SGPR pairs: the
-      // compare-and-add form serialised every code on VCC with two wait
-      // states each (decode 0.106 -> 0.099 ms with the branch-free
-      // malformed-code check and the single-step refill)
-      const int cnt = Cap - count_above<Cap>(win >> 1, lh);
-      const uint32_t e = vl[min(cnt, U) - 1];
+    };
+    auto lookup = [&]() -> uint32_t {
+      // 32 bits at p.  Bits past the end are not masked: the codes increase
+      // strictly, so they are prefix-free, and a code that fits in the bits
+      // left is found whatever follows them (one that does not fit is
+      // malformed either way)
+      const uint32_t win = (uint32_t)(acc >> 32);
+      if (use_bm) {
+        const uint32_t w8 = win >> 24, j = w8 >> 5;
+        const uint32_t row = bm[j * kLanes];
+        const uint32_t before = __builtin_amdgcn_perm(pb, pa, j | 0x0C0C0C00u);
+        const int cnt = (int)(__builtin_popcount(row >> (31 - (w8 & 31))) + before);
+        return vl[cnt - 1];
+      }
+      // borrows of win - lh[k] in two carry chains through SGPR pairs (the
+      // compare-and-add form serialised every code on VCC)
+      const uint32_t above = count_above<Cap>(win >> 1, lh);
+      return *reinterpret_cast<const uint16_t *>(vbase - (int)(above * (2 * kLanes)));
+    };
+    // one symbol at p (bits in acc): its entry; a code past the end ends the
+    // walk as malformed (flagged, no branch out of the loop per symbol)
+    auto take = [&](bool &bd) -> uint32_t {
+      const uint32_t e = lookup();
       const int L = (int)(e >> 11);
-      // a code past the end (or of length 0) ends the walk as malformed:
-      // flagged, no branch out of the loop per symbol
-      const bool badsym = p + L > nbits || L == 0;
-      bad = bad || badsym;
-      if (!badsym) put(val(e));
-      p = badsym ? nbits : p + L;
+      bd = p + L > nbits;
+      bad = bad || bd;
+      p = bd ? nbits : p + L;
       acc <<= L;
       nacc -= L;
       ++got;
+      return e;
+    };
+    // a (count, value) pair: the count, then (bits left) its value and the run
+    auto pair = [&](bool refill_each) {
+      if (refill_each) refill();
+      bool b0, b1;
+      const uint32_t e0 = take(b0);
+      if (p < nbits) {
+        if (refill_each) refill();
+        const uint32_t e1 = take(b1);
+        if (!b1) fill(val(e0), val(e1));
+      }
+    };
+    // a refill leaves >= 33 bits: four symbols when every code of the wave
+    // is <= 8 bits, two when <= 16, else one (wave-uniform cadence)
+    if (narrow) {
+      while (p < nbits) {
+        refill();
+        pair(false);
+        if (p < nbits) pair(false);
+      }
+    } else if (mid) {
+      while (p < nbits) {
+        refill();
+        pair(false);
+      }
+    } else {
+      while (p < nbits) pair(true);
     }
     if (bad || got != R) return 0;
   }
@@ -1106,86 +1210,110 @@ __device__ bool decode_stream_slow(const uint8_t *__restrict__ bits, uint32_t m,
   return true;
 }
 
-// luma and chroma waves apart, as in the encoder (their output slots
-// differ); a chroma lane decodes its tile's Cr stream, then its Cb stream
+// One wave's 64 tiles of one channel group: luma (a lane decodes its tile's
+// Y stream) or chroma (its Cr, then its Cb stream).
 template <bool kLuma>
-__global__ __launch_bounds__(kLanes) void entropy_decode_kernel(
-    const uint8_t *__restrict__ bits, const uint32_t *__restrict__ meta,
-    const uint32_t *__restrict__ table, size_t ntiles, int16_t *__restrict__ coef,
-    uint32_t *__restrict__ status) {
+__device__ __forceinline__ void decode_wave(DecLds<kLuma ? 64 : 32, kLuma ? kFastCap : kChromaCap> &S,
+                                            int lane, size_t group,
+                                            const uint8_t *__restrict__ bits,
+                                            const uint32_t *__restrict__ meta,
+                                            const uint32_t *__restrict__ table, size_t ntiles,
+                                            int16_t *__restrict__ coef,
+                                            uint32_t *__restrict__ status, uint32_t tag) {
   constexpr int Cap = kLuma ? kFastCap : kChromaCap;
-  __shared__ DecLds<kLuma ? 64 : 32, Cap> S;
-  const int lane = threadIdx.x;
-  const size_t tile = (size_t)blockIdx.x * kLanes + lane;
+  const size_t tile = group * kLanes + lane;
   if (tile >= ntiles) return;
+  uint32_t fails = 0;
   // ints are produced one at a time: collect them in LDS, then 16-B stores
   // (2-byte stores to 64 scattered streams wrote ~6x the bytes)
   int16_t *o = S.out[lane];
-  const LCol<uint16_t> vl{reinterpret_cast<uint8_t *>(&S.vl[0][lane])};
+  const VRow vl{reinterpret_cast<uint8_t *>(&S.vl[0][lane])};
 #pragma unroll 1
   for (int c = kLuma ? 0 : 1; c <= (kLuma ? 0 : 2); ++c) {
     const uint32_t m = meta[tile * 3 + c];
-    const int U = (int)(m >> 24);
     const uint8_t *b = bits + tile * kBitsPerTile + bits_off(c);
     const uint32_t *t = table + tile * kTablePerTile + bits_off(c);
+    // the table's first Cap entries and the first two 16-B chunks of the
+    // bits, loaded with the meta word (all inside the stream's slots, whatever
+    // the meta word says): one wait, where a load per code under its k < U
+    // test was waited for code by code
+    uint32_t tb[Cap];
+#pragma unroll
+    for (int i = 0; i < Cap / 4; ++i) {
+      const uint4 v = reinterpret_cast<const uint4 *>(t)[i];
+      tb[4 * i] = v.x;
+      tb[4 * i + 1] = v.y;
+      tb[4 * i + 2] = v.z;
+      tb[4 * i + 3] = v.w;
+    }
+    const uint4 q0 = reinterpret_cast<const uint4 *>(b)[0];
+    const uint4 q1 = reinterpret_cast<const uint4 *>(b)[1];
+    const int U = (int)(m >> 24);
     const int n = stream_len(c);
     // a foreign or corrupted meta word must not index past the stream's
     // slot: its bits (bits_cap bits) and its table (2 n entries: RLE of n ints)
     const bool sane = (int)(m & 0xFFFF) <= bits_cap(c) && U <= 2 * n;
     bool ok = false;
+    if (!sane)  // a use on this path too, so the loads are not sunk past the meta test
+      asm volatile("" ::"v"(tb[0]), "v"(q0.x), "v"(q1.x));
     if (sane) {
-      const int r = U <= Cap ? decode_stream<Cap>(b, m, t, vl, o, n) : -1;
+      const int r = U <= Cap ? decode_stream<Cap>(b, m, tb, q0, q1, vl, o, n,
+                                                   kLuma ? &S.bm[0][lane] : nullptr)
+                             : -1;
       ok = r < 0 ? decode_stream_slow(b, m, t, o, n) : r != 0;
     } else {
       for (int j = 0; j < n; ++j) o[j] = 0;
     }
-    if (!ok) atomicAdd(&status[1], 1u);
+    fails += !ok;
     uint4 *dst = reinterpret_cast<uint4 *>(coef + tile * 128 + coef_off(c));
     const uint32_t *src = reinterpret_cast<const uint32_t *>(o);    // 4-B aligned rows
     for (int v = 0; v < n / 8; ++v)
       dst[v] = make_uint4(src[4 * v], src[4 * v + 1], src[4 * v + 2], src[4 * v + 3]);
   }
-}
-
-// The decoder's luma and chroma kernels write disjoint outputs, and neither
-// fills the chip alone (a 4K image: 2,025 luma waves of 11.5 KB of LDS and
-// 2,025 chroma waves of 5.9 KB, each a single round of one-lane-per-stream
-// walks), so the chroma kernel runs on a side stream beside the luma one
-// (fork and join by events: the caller's stream waits for both).  One side
-// stream per device, made on first use; the mutex serialises the enqueue of
-// concurrent callers (the launches stay asynchronous).
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-constexpr int kMaxDevices = 64;
-SideStream g_side[kMaxDevices];
-std::mutex g_side_mu;
-
-// Enqueue first(s) and second(side) so that they may run concurrently and
-// everything after them on s waits for both.
-template <typename F1, typename F2>
-int run_side_by_side(hipStream_t s, F1 first, F2 second) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return JPEGR_ERR_HIP;
-  std::lock_guard<std::mutex> lock(g_side_mu);
-  SideStream &sd = g_side[dev];
-  if (!sd.s) {
-    if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess) {
-      (void)hipGetLastError();
-      return JPEGR_ERR_HIP;
-    }
+  // the wave's malformed streams, added to status[1] once workgroup 0 has
+  // zeroed it for this call (status[2] = the call's tag; see the kernel)
+  const uint32_t f = (uint32_t)__popcll(__ballot(fails & 1)) + 2u * (uint32_t)__popcll(__ballot(fails & 2));
+  if (f && lane == __builtin_ctzll(__ballot(1))) {
+    for (int spin = 0; spin < (1 << 22) &&
+                       __hip_atomic_load(&status[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != tag;
+         ++spin)
+      __builtin_amdgcn_s_sleep(2);
+    atomicAdd(&status[1], f);
   }
-  if (hipEventRecord(sd.fork, s) != hipSuccess || hipStreamWaitEvent(sd.s, sd.fork, 0) != hipSuccess)
-    return JPEGR_ERR_HIP;
-  first(s);
-  second(sd.s);
-  if (hipEventRecord(sd.join, sd.s) != hipSuccess || hipStreamWaitEvent(s, sd.join, 0) != hipSuccess)
-    return JPEGR_ERR_HIP;
-  return JPEGR_OK;
 }
+
+// A workgroup is two waves over the same 64 tiles: wave 0 decodes their luma
+// streams, wave 1 their chroma streams, each in its own LDS (12 + 6.4 KB: a
+// 4K image's 2,025 workgroups are all resident at once, a luma and a chroma
+// wave beside each other on every SIMD).  One launch: the luma and chroma
+// kernels side by side on two streams started the chroma waves 8 us late and
+// paid the fork and join.
+// status[1] is zeroed here, not by a memset ahead of the launch (a dispatch
+// and its gap): workgroup 0, dispatched first and waiting on nothing, zeroes
+// it and then publishes the call's tag in status[2]; a wave with malformed
+// streams adds them only once it reads that tag (bounded spin), so no add
+// can precede the zero.
+__global__ __launch_bounds__(2 * kLanes) void entropy_decode_kernel(
+    const uint8_t *__restrict__ bits, const uint32_t *__restrict__ meta,
+    const uint32_t *__restrict__ table, size_t ntiles, int16_t *__restrict__ coef,
+    uint32_t *__restrict__ status, uint32_t tag) {
+  __shared__ DecLds<64, kFastCap> SY;
+  __shared__ DecLds<32, kChromaCap> SC;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    status[1] = 0u;
+    __threadfence();
+    __hip_atomic_store(&status[2], tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int lane = threadIdx.x & (kLanes - 1);
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) < kLanes)
+    decode_wave<true>(SY, lane, blockIdx.x, bits, meta, table, ntiles, coef, status, tag);
+  else
+    decode_wave<false>(SC, lane, blockIdx.x, bits, meta, table, ntiles, coef, status, tag);
+}
+
+// one tag per decode call (status[2]); 0 is skipped, so a zeroed status
+// never matches
+std::atomic<uint32_t> g_decode_tag{0};
 
 }  // namespace
 
@@ -1224,28 +1352,17 @@ extern "C" int jpegr_entropy_decode_device(const void *d_bits, const void *d_met
                                            void *d_status, void *stream) {
   if (!d_bits || !d_meta || !d_table || !d_coef || !d_status || ntiles == 0 ||
       ntiles > ((size_t)1 << 32) / 3 || (reinterpret_cast<uintptr_t>(d_coef) & 15) != 0 ||
-      (reinterpret_cast<uintptr_t>(d_bits) & 15) != 0)
+      (reinterpret_cast<uintptr_t>(d_bits) & 15) != 0 ||
+      (reinterpret_cast<uintptr_t>(d_table) & 15) != 0 ||
+      (reinterpret_cast<uintptr_t>(d_status) & 3) != 0)
     return JPEGR_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(static_cast<uint32_t *>(d_status) + 1, 0, sizeof(uint32_t), s) != hipSuccess)
-    return JPEGR_ERR_HIP;
+  uint32_t tag = ++g_decode_tag;
+  if (tag == 0) tag = ++g_decode_tag;
   const unsigned groups = (unsigned)((ntiles + kLanes - 1) / kLanes);
-  const int rc = run_side_by_side(
-      s,
-      [&](hipStream_t q) {
-        hipLaunchKernelGGL(entropy_decode_kernel<true>, dim3(groups), dim3(kLanes), 0, q,
-                           static_cast<const uint8_t *>(d_bits),
-                           static_cast<const uint32_t *>(d_meta),
-                           static_cast<const uint32_t *>(d_table), ntiles,
-                           static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
-      },
-      [&](hipStream_t q) {
-        hipLaunchKernelGGL(entropy_decode_kernel<false>, dim3(groups), dim3(kLanes), 0, q,
-                           static_cast<const uint8_t *>(d_bits),
-                           static_cast<const uint32_t *>(d_meta),
-                           static_cast<const uint32_t *>(d_table), ntiles,
-                           static_cast<int16_t *>(d_coef), static_cast<uint32_t *>(d_status));
-      });
-  if (rc != JPEGR_OK) return rc;
+  hipLaunchKernelGGL(entropy_decode_kernel, dim3(groups), dim3(2 * kLanes), 0, s,
+                     static_cast<const uint8_t *>(d_bits), static_cast<const uint32_t *>(d_meta),
+                     static_cast<const uint32_t *>(d_table), ntiles, static_cast<int16_t *>(d_coef),
+                     static_cast<uint32_t *>(d_status), tag);
   return hipGetLastError() == hipSuccess ? JPEGR_OK : JPEGR_ERR_HIP;
 }

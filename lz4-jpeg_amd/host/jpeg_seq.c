@@ -73,7 +73,8 @@ int main(int argc, char **argv) {
       hipMalloc(&d_meta, ntiles * 3 * 4) != hipSuccess ||
       hipMalloc(&d_table, ntiles * 256 * 4) != hipSuccess ||
       hipMalloc(&d_scr, jpegr_entropy_scratch_bytes(ntiles)) != hipSuccess ||
-      hipMalloc(&d_st, 8) != hipSuccess)
+      hipMalloc(&d_st, 16) != hipSuccess ||
+      hipMemset(d_st, 0, 16) != hipSuccess)
     fail("device allocation failed");
   if (hipMemcpy(d_rgba, rgba, npx * 4, hipMemcpyHostToDevice) != hipSuccess) fail("copy in");
   if (jpegr_planes_device(d_rgba, w, h, d_y, d_cr, d_cb, NULL) != JPEGR_OK ||

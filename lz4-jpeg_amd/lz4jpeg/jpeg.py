@@ -96,7 +96,8 @@ def reconstruct_device(d_coef, w, h, nimg=1, d_orig=None, stream=None):
 class Entropy:
     """Device buffers of the entropy stage for `ntiles` tiles (all images):
     bits (256 B/tile), meta (3 u32/tile), table (256 u32/tile), scratch and
-    the 2-word status (see jpegr.h)."""
+    the status words (see jpegr.h: [0] encode, [1] decode, [2] the decoder's
+    call tag)."""
 
     def __init__(self, ntiles, device="cuda"):
         import torch
@@ -106,7 +107,7 @@ class Entropy:
         self.table = torch.zeros(ntiles * 256, dtype=torch.int32, device=device)
         nscr = _lib.lib().jpegr_entropy_scratch_bytes(ntiles)
         self.scratch = torch.empty(nscr, dtype=torch.uint8, device=device)
-        self.status = torch.zeros(2, dtype=torch.int32, device=device)
+        self.status = torch.zeros(4, dtype=torch.int32, device=device)
 
     def encode(self, d_coef, stream=None):
         """RLE + per-stream Huffman + encoded bits of every stream

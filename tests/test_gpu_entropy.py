@@ -186,3 +186,51 @@ def test_fast_path_boundaries(gpu, oracle):
     torch.cuda.synchronize()
     assert int(ent.status[1].item()) == 0
     assert torch.equal(out, d_coef)
+
+
+def test_decode_counts_malformed_streams(gpu, oracle):
+    """status[1] counts exactly the malformed streams of one call -- truncated
+    bits (nbits - 1), a wrong RLE length, a meta word past the slot -- in
+    workgroup 0 and later ones, is not carried into the next call, and the
+    other streams still decode (the decoder zeroes status[1] itself; the
+    call's tag in status[2] orders the adds after the zero)."""
+    import torch
+    from lz4jpeg import jpeg
+    w, h = 512, 384
+    img = oracle.rand_image(w, h, seed=5)
+    d_coef = jpeg.encode_device(torch.from_numpy(img).cuda(), w, h)
+    nt = jpeg.tiles(w, h)
+    ent = jpeg.Entropy(nt)
+    ent.encode(d_coef)
+    torch.cuda.synchronize()
+    clean = ent.meta.clone()
+    meta = clean.cpu().numpy().view(np.uint32).reshape(nt, 3).copy()
+    nbits, rle, ncodes = meta & 0xFFFF, (meta >> 16) & 255, meta >> 24
+    bad = set()
+    for t in (0, 1, 63, 64, 777, nt - 1):                  # truncated luma bits
+        assert ncodes[t, 0] > 1 and nbits[t, 0] > 1
+        meta[t, 0] -= 1
+        bad.add((t, 0))
+    for t in (2, 65, 1500, nt - 2):                        # Cr: two RLE ints too many
+        assert ncodes[t, 1] > 1
+        meta[t, 1] += 2 << 16
+        bad.add((t, 1))
+    for t in (3, 2000):                                    # Cb: bits past its slot
+        meta[t, 2] = (meta[t, 2] & ~np.uint32(0xFFFF)) | np.uint32(600)
+        bad.add((t, 2))
+    ent.meta.copy_(torch.from_numpy(meta.reshape(-1).view(np.int32)))
+    coef = d_coef.view(nt, 128)
+    for _ in range(2):                                     # not accumulated over calls
+        out = torch.zeros_like(d_coef)
+        ent.decode(out)
+        torch.cuda.synchronize()
+        assert int(ent.status[1].item()) == len(bad)
+        ok_rows = torch.ones(nt, dtype=torch.bool, device="cuda")
+        ok_rows[sorted({t for t, _ in bad})] = False
+        assert torch.equal(out.view(nt, 128)[ok_rows], coef[ok_rows])
+    ent.meta.copy_(clean)
+    out = torch.zeros_like(d_coef)
+    ent.decode(out)
+    torch.cuda.synchronize()
+    assert int(ent.status[1].item()) == 0
+    assert torch.equal(out, d_coef)
