@@ -884,7 +884,7 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
 // u16 (value in 11 bits, two's complement, | length << 11: every value of a
 // 4K image's streams fits; a stream whose values or lengths do not takes the
 // slow path), one row of u16 per code.  With the decoded ints and the luma
-// start map: 13.6 KB per luma wave, 5.9 KB per chroma wave (a lane decodes
+// start map: 13.3 KiB per luma wave, 6.0 KiB per chroma wave (a lane decodes
 // the tile's Cr, then its Cb stream), one of each per workgroup: a 4K image's
 // 2,025 workgroups are all resident at once.
 template <int N, int Cap>
