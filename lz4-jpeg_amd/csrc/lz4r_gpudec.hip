@@ -23,7 +23,10 @@
 //   - the lane reads its encoded bytes with single unaligned 8/16-byte
 //     global loads (L1/L2 absorb the re-reads of the wave's ~20 KB range),
 //     after touching the block's next four 128-B lines up front so that the
-//     serial walk does not wait on HBM once per line;
+//     serial walk does not wait on HBM once per line; a sequence's distance
+//     word, two literal chunks and the next window are issued together, so
+//     the walk waits on memory once per sequence (a load per chunk, each
+//     waited for, cost 1.28 -> 1.18 ms per GiB: tools/r06_r.sh);
 //   - literals move in 16-byte chunks; a match of distance D is copied in
 //     chunks of min(16, d) bytes at a distance d that grows from D (the
 //     match is D-periodic, so any multiple of D up to the bytes already
@@ -423,8 +426,20 @@ __device__ __forceinline__ int decode_block_plain(const BytesT &p, int len, bool
     const bool oks = Sz == L + 5 + mx;
     bool okp = (big & okb) | (!big & oks);
     const int lit = ip + 3 + le;
-    okp = okp && ip + 3 <= len && ip - 3 + Sz <= want && lit + L + 2 <= len && pos + L <= kBlk;
+    // (bitwise & and |: every test is evaluated, no short-circuit branches;
+    // the size-field sum is checked once, after the walk: ip - 3 == want;
+    // lit + L + 2 <= len keeps this sequence's reads inside the stream)
+    okp = okp & (ip + 3 <= len) & (lit + L + 2 <= len) & (pos + L <= kBlk);
     const int nip = lit + L + 2 + mx;
+    // the distance word and the two literal chunks past the window, loaded
+    // together: one wait where a long literal run waited for the distance
+    // word, then for each chunk (all inside the stream: the plain path runs
+    // only with kInMax + 64 bytes after the block); the next window last, so
+    // that waiting for these (vmcnt counts in issue order) does not wait for it
+    const int wl = min(L, ip + 16 - lit);
+    const int lb = okp ? lit + wl : ip;
+    const uint32_t tw = (uint32_t)p.ld8(okp ? lit + L : 0);
+    const V16 c1 = p.ld16(lb), c2 = p.ld16(lb + 16);
     const V16 hn = p.ld16(okp ? nip : ip);           // next window, in flight during the copies
     const int off = lit + L - ip;                    // distance bytes within the window?
     uint32_t t;
@@ -434,19 +449,27 @@ __device__ __forceinline__ int decode_block_plain(const BytesT &p, int len, bool
       const uint32_t c = wi == 0 ? w1 : wi == 1 ? w2 : w3;
       t = __builtin_amdgcn_alignbyte(c, a, (uint32_t)off & 3u);
     }
-    if (off + 3 > 16) t = (uint32_t)p.ld8(okp ? lit + L : 0);
+    if (off + 3 > 16) t = tw;
     const int D = (int)(t & 0xFFFF);
     const bool hasm = D != 0;
-    const int M = hasm ? (mx ? 19 + (int)((t >> 16) & 255) : tm + 4) : 0;
-    okp = okp && (hasm ? (nip <= len && D <= pos + L && pos + L + M <= kBlk)
-                       : (k + 1 == nseq && tm == 0));   // literal-only tail, LZ4.c:585-613
+    const int Mx = 19 + (int)((t >> 16) & 255), Ms = tm + 4;
+    const int M = hasm ? (mx ? Mx : Ms) : 0;
+    const bool mok = (nip <= len) & (D <= pos + L) & (pos + L + M <= kBlk);
+    const bool tailok = (k + 1 == nseq) & (tm == 0);   // literal-only tail, LZ4.c:585-613
+    okp = okp & ((hasm & mok) | (!hasm & tailok));
     if (!okp) {
+      // a use of the chunks and the next window on this path too, so that
+      // their loads are not sunk below this test (issued apart, they would be
+      // waited for apart)
+      asm volatile("" ::"v"(c1.lo), "v"(c1.hi), "v"(c2.lo), "v"(c2.hi), "v"(hn.lo), "v"(hn.hi));
       bad = true;
       break;
     }
-    // literals: the window's bytes, then 16 at a time from the stream
-    const int wl = min(L, ip + 16 - lit);
-    if (wl > 0) {
+    // literals: the window's bytes, the two chunks, then 16 at a time.  The
+    // first two stores are unconditional: they stay inside the slot and its
+    // slack (pos + wl <= pos + L <= 300), and what they write past the run is
+    // overwritten by the match or the next sequence before anything reads it
+    {
       // the window from byte d = lit - ip (3, 4 or 5): dwords from w[d >> 2]
       const bool d4 = le > 0;                         // d = 3 + le
       const uint32_t sh = (uint32_t)(3 + le) & 3u;
@@ -457,11 +480,15 @@ __device__ __forceinline__ int decode_block_plain(const BytesT &p, int len, bool
       const uint32_t o3 = __builtin_amdgcn_alignbyte(0u, s3, sh);
       o.st_fast(pos, {(uint64_t)o1 << 32 | o0, (uint64_t)o3 << 32 | o2}, wl);
     }
-    for (int i = wl; i < L; i += 16) o.st_fast(pos + i, p.ld16(lit + i), min(16, L - i));
-    // match: one 16-B piece when it neither overlaps itself nor exceeds 16
+    o.st_fast(pos + wl, c1, min(16, L - wl));
+    if (L > wl + 16) o.st_fast(pos + wl + 16, c2, min(16, L - wl - 16));
+    for (int i = wl + 32; i < L; i += 16) o.st_fast(pos + i, p.ld16(lit + i), min(16, L - i));
+    // match: one 16-B piece, unconditionally (with no match it writes inside
+    // the slot's slack what the next sequence overwrites), then the general
+    // copy when the match overlaps itself or exceeds 16 bytes
     const int q = pos + L;
-    if (M > 0 && M <= 16 && D >= 16) o.st_fast(q, o.ld16(q - D), M);
-    else if (M > 0) copy_match(o, q, D, M);
+    o.st_fast(q, o.ld16(q - D), M);
+    if ((M > 16) | ((M > 0) & (D < 16))) copy_match(o, q, D, M);
     ++k;
     ip = nip;
     h = hn;
