@@ -4,8 +4,9 @@
 
 The product library compresses the 1 GiB bench corpus once; every build
 (its own ctypes handle, RTLD_LOCAL) then decodes it with the compressor's
-device-resident block offsets (lz4r_decompress_device), round-robin after
-30 warm-up calls.  Kernel time from torch events on the current stream;
+device-resident block offsets (lz4r_decompress_device; DEC_MODE=bare: the
+stream alone, lz4r_decompress_stream_device), round-robin after 30 warm-up
+calls.  Kernel time from torch events on the current stream;
 every build's output is compared with the input once."""
 import ctypes
 import os
@@ -36,7 +37,18 @@ def main():
     d_res = torch.zeros(2, dtype=torch.int64, device="cuda")
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
+    bare = os.environ.get("DEC_MODE") == "bare"
+    got = ctypes.c_size_t(0)
+
     def dec(lib):
+        if bare:                  # the stream alone (lz4r_decompress_stream_device, synchronous)
+            rc = lib.lz4r_decompress_stream_device(ctypes.c_void_p(d_stream.data_ptr()),
+                                                   ctypes.c_size_t(length),
+                                                   ctypes.c_void_p(d_out.data_ptr()),
+                                                   ctypes.c_size_t(n + 300), ctypes.byref(got), stream)
+            assert rc == 0 and got.value == n, (rc, got.value)
+            d_res[0] = n
+            return
         rc = lib.lz4r_decompress_device(ctypes.c_void_p(d_stream.data_ptr()), ctypes.c_size_t(length),
                                         ctypes.c_void_p(d_offs), ctypes.c_size_t(nb),
                                         ctypes.c_void_p(d_out.data_ptr()), ctypes.c_size_t(n + 300),

@@ -10,4 +10,8 @@ for v in $1; do
   echo "$v: $(tail -1 $O/tests_$v.log)"
 done
 libs=""; for v in $2; do [ $v = prod ] && libs="$libs prod" || libs="$libs $A/liblz4r_gpudec_$v.so"; done
-timeout -k 10 300 python -u tools/ab_dec_inproc.py 20 $libs $libs > $O/ab.log 2>&1; rc=$?; tail -12 $O/ab.log; exit $rc
+timeout -k 10 300 python -u tools/ab_dec_inproc.py 20 $libs $libs > $O/ab.log 2>&1; rc=$?; tail -12 $O/ab.log
+[ $rc = 0 ] || exit $rc
+[ -n "$3" ] || exit 0
+libs=""; for v in $3; do [ $v = prod ] && libs="$libs prod" || libs="$libs $A/liblz4r_gpudec_$v.so"; done
+DEC_MODE=bare timeout -k 10 300 python -u tools/ab_dec_inproc.py 10 $libs $libs > $O/ab_bare.log 2>&1; rc=$?; tail -8 $O/ab_bare.log; exit $rc
