@@ -397,7 +397,9 @@ __device__ __forceinline__ bool tree_codes(const W &w, int U, uint32_t *__restri
       pcode = d >= plen ? t << (d - plen) : t >> (plen - d);
       plen = d;
       if (k < U) {
-        w.code[x] = pcode | (uint32_t)d << 24;        // depth <= Cap - 1 < 24
+        // the code left-aligned, its length in the low 5 bits (depth <= Cap - 1
+        // < 27 leaves them zero)
+        w.code[x] = (d ? pcode << (32 - d) : 0u) | (uint32_t)d;
         table[k] = (uint16_t)sy[k] | ((uint32_t)d << 16);
       }
     }
@@ -622,7 +624,7 @@ struct WCol {
 
 template <class HeapCol>
 struct LaneWork {                                     // the arrays tree_codes uses
-  static constexpr bool kPackLen = true;              // code | length << 24, one read
+  static constexpr bool kPackLen = true;              // code and length in one dword (tree_codes)
   static constexpr bool kTopDown = true;              // codes top-down over mrec (tree_codes)
   LCol<int8_t> sym;
   HeapCol heap;
@@ -775,15 +777,27 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
     bool over = tree_codes<Cap>(w, U, table + tile * kTablePerTile + bits_off(c), h0);
 
     // ---- encoded sequence, MSB-first (JPEG.c:993-1007) ------------------------
-    uint32_t *const wout = reinterpret_cast<uint32_t *>(bits + tile * kBitsPerTile + bits_off(c));
+    uint8_t *const sout = bits + tile * kBitsPerTile + bits_off(c);
     constexpr int nwords = N / 2;                       // bits_cap / 32
-    // A leaf's code and length are one dword (code | length << 24); the reads
-    // do not depend on the bit accumulator, so each group of kG positions'
-    // code words is read while the previous group is shifted in.
+    // A leaf's code word is its code left-aligned with its length in the low
+    // 5 bits; the reads do not depend on the bit position, so each group of
+    // kG positions' code words is read while the previous group is placed.
+    // Each code is or-ed into the lane's zeroed bit rows at its bit position
+    // (two ds_or: the word it starts in and the next), the rows past the code
+    // table through the dead heap and symbols; two spill rows take the bits of
+    // a stream that overflows its slot.  No exec branch per code: the
+    // accumulator form stored each completed word under one.
     const LCol<uint32_t> codez{colp(&S.tab[L::ZeroRow][0])};
+    constexpr int BitRow = L::CodeRow + Cap;
+    static_assert(BitRow + nwords + 2 <= Keys / 4 + L::HeapRows + Cap / 4 &&
+                      offsetof(L, heap) == sizeof(S.tab) && offsetof(L, sym) == offsetof(L, heap) + sizeof(S.heap),
+                  "the bit rows fit the dead rows past the codes");
+    uint8_t *const brow = reinterpret_cast<uint8_t *>(&S) + BitRow * (4 * kLanes) + 4 * lane;
+    auto bit_row = [&](int r) { return reinterpret_cast<uint32_t *>(brow + r * (4 * kLanes)); };
     codez[0] = 0u;
-    uint64_t acc = 0;
-    int nacc = 0, word = 0;
+#pragma unroll
+    for (int r = 0; r < nwords + 2; ++r) *bit_row(r) = 0u;
+    int pos = 0;
     constexpr int kG = 4;
     static_assert(N % kG == 0, "whole groups");
     auto ident = [&](int i, int h) {                    // leaf + 1 of emission h at position i, 0: none
@@ -804,18 +818,30 @@ __global__ __launch_bounds__(kLanes) void entropy_encode_lane(
       if (g + 1 < N / kG) fetch(g + 1, nxt);
 #pragma unroll
       for (int j = 0; j < 2 * kG; ++j) {
-        const int Lb = (int)(cur[j] >> 24);
-        acc = (acc << Lb) | (cur[j] & 0xFFFFFFu);
-        nacc += Lb;
-        const bool full = nacc >= 32;
-        nacc -= full ? 32 : 0;
-        if (full && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc >> nacc));
-        word += full ? 1 : 0;
+        const uint32_t al = cur[j] & ~31u;
+        const uint32_t o = (uint32_t)pos & 31u;
+        uint32_t *const r0 = bit_row(min(pos >> 5, nwords));
+        atomicOr(r0, al >> o);
+        atomicOr(r0 + kLanes, __builtin_amdgcn_alignbit(al, 0u, o));   // (o = 0: none)
+        pos += (int)(cur[j] & 31u);
       }
     }
-    const int nbits = 32 * word + nacc;
-    if (nacc && word < nwords) wout[word] = __builtin_bswap32((uint32_t)(acc << (32 - nacc)));
+    const int nbits = pos;
     if (nbits > ref_bits_max(c)) over = true;           // char sequence[1024] / [512]
+    // the slot's words, MSB-first bytes (16-B stores when the slot is aligned)
+    {
+      uint32_t wv[nwords];
+#pragma unroll
+      for (int r = 0; r < nwords; ++r) wv[r] = __builtin_bswap32(*bit_row(r));
+      if ((reinterpret_cast<uintptr_t>(bits) & 15u) == 0) {
+#pragma unroll
+        for (int k = 0; k < nwords / 4; ++k)
+          reinterpret_cast<uint4 *>(sout)[k] = make_uint4(wv[4 * k], wv[4 * k + 1], wv[4 * k + 2], wv[4 * k + 3]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < nwords; ++r) reinterpret_cast<uint32_t *>(sout)[r] = wv[r];
+      }
+    }
     meta[tile * 3 + c] = (uint32_t)(nbits < 0xFFFF ? nbits : 0xFFFF) | ((uint32_t)R << 16) |
                          ((uint32_t)U << 24);
     if constexpr (kLuma) {
