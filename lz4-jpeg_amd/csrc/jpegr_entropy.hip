@@ -587,8 +587,9 @@ struct LaneLds {
   static constexpr int Keys = N == 64 ? 176 : 120;   // symbols [-Off, Keys - Off)
   static constexpr int Off = N == 64 ? 64 : 48;       // counts: 1 .. N
   static constexpr int StkRows = (Cap + 2) / 2;       // overlays of the table (dword rows)
-  // a zero row, then code | length << 24 per leaf (leaf + 1 indexes from the
-  // zero row: id 0, no emission, reads a length-0 code)
+  // a zero row, then per leaf its code left-aligned | length (leaf + 1
+  // indexes from the zero row: id 0, no emission, reads a length-0 code);
+  // past the codes, the sequence pass's bit rows (through heap and sym)
   static constexpr int ZeroRow = StkRows, CodeRow = StkRows + 1;
   static_assert(CodeRow + Cap <= Keys / 4, "stack and codes fit the table");
   // (the merge records, Cap - 1 rows from row 0, are dead before the codes
