@@ -109,7 +109,8 @@ const char *jpegr_strerror(int code);
  * :964), and the encoded sequence (:993).  Output per tile (ntiles = all
  * tiles of all images):
  *   d_bits   256 B: [Y 128][Cr 64][Cb 64] bytes, bits packed MSB-first
- *            (the reference's '0'/'1' chars)
+ *            (the reference's '0'/'1' chars); the final byte's unused low
+ *            bits are 0, bytes past it unspecified
  *   d_meta   3 u32 (Y, Cr, Cb): nbits | rle_len << 16 | ncodes << 24
  *   d_table  256 u32: [Y 128][Cr 64][Cb 64]; entry k = value (int16) |
  *            code length << 16, in the reference's codes[] (DFS) order;
