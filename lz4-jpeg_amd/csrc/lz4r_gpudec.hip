@@ -26,7 +26,11 @@
 //     serial walk does not wait on HBM once per line; a sequence's distance
 //     word, two literal chunks and the next window are issued together, so
 //     the walk waits on memory once per sequence (a load per chunk, each
-//     waited for, cost 1.28 -> 1.18 ms per GiB: tools/r06_r.sh);
+//     waited for, cost 1.28 -> 1.18 ms per GiB: tools/r06_r.sh), and each of
+//     them only on the lanes that need it: the vector memory address unit is
+//     the bound (TA busy ~80 % of the kernel, ~45 cycles per scattered wave
+//     load, tools/r06_w.sh), and a lane with exec off costs it nothing
+//     (1.17 -> 1.06 ms per GiB);
 //   - literals move in 16-byte chunks; a match of distance D is copied in
 //     chunks of min(16, d) bytes at a distance d that grows from D (the
 //     match is D-periodic, so any multiple of D up to the bytes already
@@ -437,11 +441,16 @@ __device__ __forceinline__ int decode_block_plain(const BytesT &p, int len, bool
     // only with kInMax + 64 bytes after the block); the next window last, so
     // that waiting for these (vmcnt counts in issue order) does not wait for it
     const int wl = min(L, ip + 16 - lit);
-    const int lb = okp ? lit + wl : ip;
-    const uint32_t tw = (uint32_t)p.ld8(okp ? lit + L : 0);
-    const V16 c1 = p.ld16(lb), c2 = p.ld16(lb + 16);
-    const V16 hn = p.ld16(okp ? nip : ip);           // next window, in flight during the copies
     const int off = lit + L - ip;                    // distance bytes within the window?
+    // each load only on the lanes that need it: the vector memory address
+    // unit is the decoder's bound (TA busy ~80 % of the kernel, ~45 cycles
+    // per scattered wave load), and a lane with exec off costs it nothing
+    uint32_t tw = 0;
+    V16 c1 = {0, 0}, c2 = {0, 0};
+    if (okp & (off + 3 > 16)) tw = (uint32_t)p.ld8(lit + L);
+    if (okp & (L > wl)) c1 = p.ld16(lit + wl);
+    if (okp & (L > wl + 16)) c2 = p.ld16(lit + wl + 16);
+    const V16 hn = p.ld16(okp ? nip : ip);           // next window, in flight during the copies
     uint32_t t;
     {
       const int wi = off >> 2;
