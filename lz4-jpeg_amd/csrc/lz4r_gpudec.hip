@@ -731,8 +731,14 @@ __global__ __launch_bounds__(256) void lz4_bare_cand(const uint8_t *__restrict__
 template <bool kExact>
 __device__ __forceinline__ int bare_block_len(const uint8_t *in, size_t in_len, size_t x) {
   if (x + 3 > in_len) return 0;
-  const int size = (int)in[x + 1] | ((int)in[x + 2] << 8);
-  if (!kExact) return in[x] >= 1 && size >= 8 && size <= kInMax && x + size <= in_len ? size : 0;
+  if (!kExact) {
+    // the header as one unaligned dword load (three byte loads were three
+    // scattered wave loads for the vector memory address unit)
+    const uint32_t h = x + 4 <= in_len ? *reinterpret_cast<const u32u *>(in + x)
+                                       : (uint32_t)in[x] | (uint32_t)in[x + 1] << 8 | (uint32_t)in[x + 2] << 16;
+    const int size = (int)((h >> 8) & 0xFFFF);
+    return (h & 255) >= 1 && size >= 8 && size <= kInMax && x + size <= in_len ? size : 0;
+  }
   const size_t rem = in_len - x;
   const int len = rem < (size_t)kInMax ? (int)rem : kInMax;
   return decode_block<Bytes<true>, NullSlot, true>(Bytes<true>{in + x, rem}, len,

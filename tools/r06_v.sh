@@ -14,4 +14,4 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prod -o run -- python3 
 for v in $1; do
   LZ4JPEG_LIB=$A/liblz4r_gpudec_$v.so timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/$v -o run -- python3 tools/dec_one.py 1073741824 5 > $O/$v.log 2>&1 || exit 1
 done
-for v in prod $1; do echo "== $v"; python3 tools/prof_summary.py $O/$v | grep -E "bare_cand|decode_blocks"; done
+for v in prod $1; do echo "== $v"; python3 tools/prof_summary.py $O/$v | grep -E "bare|decode_blocks"; done
