@@ -24,13 +24,15 @@
 //     global loads (L1/L2 absorb the re-reads of the wave's ~20 KB range),
 //     after touching the block's next four 128-B lines up front so that the
 //     serial walk does not wait on HBM once per line; a sequence's distance
-//     word, two literal chunks and the next window are issued together, so
-//     the walk waits on memory once per sequence (a load per chunk, each
-//     waited for, cost 1.28 -> 1.18 ms per GiB: tools/r06_r.sh), and each of
-//     them only on the lanes that need it: the vector memory address unit is
-//     the bound (TA busy ~80 % of the kernel, ~45 cycles per scattered wave
-//     load, tools/r06_w.sh), and a lane with exec off costs it nothing
-//     (1.17 -> 1.06 ms per GiB);
+//     word, up to four literal chunks past the window and the next window
+//     are issued together, so the walk waits on memory once per sequence of
+//     up to ~77 literals (a load per chunk, each waited for, cost 1.28 ->
+//     1.18 ms per GiB: tools/r06_r.sh; two chunks instead of four, 1.068 ->
+//     1.015), longer runs take four chunks per round trip, and each load runs
+//     only on the lanes that need it: the vector memory address unit is the
+//     bound (TA busy ~80 % of the kernel, ~45 cycles per scattered wave load,
+//     tools/r06_w.sh), and a lane with exec off costs it nothing (1.17 ->
+//     1.06 ms per GiB);
 //   - literals move in 16-byte chunks; a match of distance D is copied in
 //     chunks of min(16, d) bytes at a distance d that grows from D (the
 //     match is D-periodic, so any multiple of D up to the bytes already
@@ -435,7 +437,7 @@ __device__ __forceinline__ int decode_block_plain(const BytesT &p, int len, bool
     // lit + L + 2 <= len keeps this sequence's reads inside the stream)
     okp = okp & (ip + 3 <= len) & (lit + L + 2 <= len) & (pos + L <= kBlk);
     const int nip = lit + L + 2 + mx;
-    // the distance word and the two literal chunks past the window, loaded
+    // the distance word and up to four literal chunks past the window, loaded
     // together: one wait where a long literal run waited for the distance
     // word, then for each chunk (all inside the stream: the plain path runs
     // only with kInMax + 64 bytes after the block); the next window last, so
@@ -446,10 +448,12 @@ __device__ __forceinline__ int decode_block_plain(const BytesT &p, int len, bool
     // unit is the decoder's bound (TA busy ~80 % of the kernel, ~45 cycles
     // per scattered wave load), and a lane with exec off costs it nothing
     uint32_t tw = 0;
-    V16 c1 = {0, 0}, c2 = {0, 0};
+    V16 c1 = {0, 0}, c2 = {0, 0}, c3 = {0, 0}, c4 = {0, 0};
     if (okp & (off + 3 > 16)) tw = (uint32_t)p.ld8(lit + L);
     if (okp & (L > wl)) c1 = p.ld16(lit + wl);
     if (okp & (L > wl + 16)) c2 = p.ld16(lit + wl + 16);
+    if (okp & (L > wl + 32)) c3 = p.ld16(lit + wl + 32);
+    if (okp & (L > wl + 48)) c4 = p.ld16(lit + wl + 48);
     const V16 hn = p.ld16(okp ? nip : ip);           // next window, in flight during the copies
     uint32_t t;
     {
@@ -470,7 +474,8 @@ __device__ __forceinline__ int decode_block_plain(const BytesT &p, int len, bool
       // a use of the chunks and the next window on this path too, so that
       // their loads are not sunk below this test (issued apart, they would be
       // waited for apart)
-      asm volatile("" ::"v"(c1.lo), "v"(c1.hi), "v"(c2.lo), "v"(c2.hi), "v"(hn.lo), "v"(hn.hi));
+      asm volatile("" ::"v"(c1.lo), "v"(c1.hi), "v"(c2.lo), "v"(c2.hi), "v"(c3.lo), "v"(c3.hi),
+                   "v"(c4.lo), "v"(c4.hi), "v"(hn.lo), "v"(hn.hi));
       bad = true;
       break;
     }
@@ -491,7 +496,21 @@ __device__ __forceinline__ int decode_block_plain(const BytesT &p, int len, bool
     }
     o.st_fast(pos + wl, c1, min(16, L - wl));
     if (L > wl + 16) o.st_fast(pos + wl + 16, c2, min(16, L - wl - 16));
-    for (int i = wl + 32; i < L; i += 16) o.st_fast(pos + i, p.ld16(lit + i), min(16, L - i));
+    if (L > wl + 32) o.st_fast(pos + wl + 32, c3, min(16, L - wl - 32));
+    if (L > wl + 48) o.st_fast(pos + wl + 48, c4, min(16, L - wl - 48));
+    // longer runs: four chunks per memory round trip (loaded on the lanes
+    // that need each, then stored), not one
+    for (int i = wl + 64; i < L; i += 64) {
+      V16 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = {0, 0};
+        if (i + 16 * j < L) v[j] = p.ld16(lit + i + 16 * j);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (i + 16 * j < L) o.st_fast(pos + i + 16 * j, v[j], min(16, L - i - 16 * j));
+    }
     // match: one 16-B piece, unconditionally (with no match it writes inside
     // the slot's slack what the next sequence overwrites), then the general
     // copy when the match overlaps itself or exceeds 16 bytes
