@@ -174,7 +174,9 @@ int lz4r_decompress_device(const void *d_in, size_t in_len, const void *d_block_
  * One host read-back per pass when out_cap / 300 + 1 <= (in_len - 1) / 8 + 1
  * (the output bounds the block count); a larger out_cap reads the block
  * count back first.  Device scratch: ~20 B per 4 KiB of stream + 8 B per
- * block out_cap can hold (stream-ordered allocation, freed on return). */
+ * block out_cap can hold (stream-ordered allocation from a per-device pool
+ * the library keeps: returned to the pool on return, not to the device, so
+ * the next call does not map it again). */
 int lz4r_decompress_stream_device(const void *d_in, size_t in_len, void *d_out,
                                   size_t out_cap, size_t *out_len, void *stream);
 

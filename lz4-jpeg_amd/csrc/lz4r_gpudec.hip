@@ -61,6 +61,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 #include "../../include/lz4r.h"
 
@@ -1053,6 +1055,35 @@ namespace {
 
 // one pass of the bare-stream decode in mode kExact; returns LZ4R_OK, or
 // LZ4R_ERR_CORRUPT when the chain or a block does not hold together.  With
+// The bare path's per-call scratch comes from a pool of the library's own
+// per device that keeps its memory (release threshold: all): from the
+// default pool, whose threshold is 0, every call re-mapped its ~34 MB per GiB
+// of stream after the previous call's synchronise returned it.
+hipMemPool_t scratch_pool() {
+  static std::mutex mu;
+  static std::map<int, hipMemPool_t> pools;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = pools.find(dev);
+  if (it != pools.end()) return it->second;
+  hipMemPoolProps props = {};
+  props.allocType = hipMemAllocationTypePinned;
+  props.location.type = hipMemLocationTypeDevice;
+  props.location.id = dev;
+  hipMemPool_t p = nullptr;
+  if (hipMemPoolCreate(&p, &props) != hipSuccess) return nullptr;
+  uint64_t keep = ~0ull;
+  (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+  pools[dev] = p;
+  return p;
+}
+
+hipError_t scratch_alloc(void **ptr, size_t bytes, hipStream_t s) {
+  hipMemPool_t p = scratch_pool();
+  return p ? hipMallocFromPoolAsync(ptr, bytes, p, s) : hipMallocAsync(ptr, bytes, s);
+}
+
 // boff given (nb_cap of them: the most blocks out_cap can hold), one host
 // read-back: the block count stays on the device, the decoder's grid is sized
 // for nb_cap and lz4_bare_gate decides on the device whether anything is
@@ -1083,7 +1114,7 @@ int bare_pass(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap, si
       return LZ4R_ERR_HIP;
     if (h2[1] != 0 || h2[0] == 0) return LZ4R_ERR_CORRUPT;
     nb_cap = (size_t)h2[0];
-    if (hipMallocAsync(reinterpret_cast<void **>(&own), nb_cap * sizeof(uint64_t), s) !=
+    if (scratch_alloc(reinterpret_cast<void **>(&own), nb_cap * sizeof(uint64_t), s) !=
         hipSuccess)
       return LZ4R_ERR_NOMEM;
     boff = own;
@@ -1140,7 +1171,7 @@ extern "C" int lz4r_decompress_stream_device(const void *d_in, size_t in_len, vo
   const size_t o_boff = al16(o_lst + 2 * (size_t)kList * nchunks);
   const size_t bytes = o_boff + 8 * nb_cap;
   uint8_t *scr = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void **>(&scr), bytes, s) != hipSuccess) return LZ4R_ERR_NOMEM;
+  if (scratch_alloc(reinterpret_cast<void **>(&scr), bytes, s) != hipSuccess) return LZ4R_ERR_NOMEM;
   uint64_t *cand = reinterpret_cast<uint64_t *>(scr);
   uint64_t *exitp = cand + nchunks;
   unsigned long long *gsum = reinterpret_cast<unsigned long long *>(scr + o_gsum);
