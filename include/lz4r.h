@@ -161,7 +161,7 @@ int lz4r_decompress_device(const void *d_in, size_t in_len, const void *d_block_
 
 /* Decode a bare framed stream on the GPU -- only the stream, as LZ4_decode
  * (LZ4.c:1038) takes the file: the block boundaries are found on the device
- * (csrc/lz4r_gpudec.hip: a candidate header per 4 KiB chunk, a lane per
+ * (csrc/lz4r_gpudec.hip: a candidate header per 8 KiB chunk, a lane per
  * chunk walking the size fields, one wave re-walking any chunk whose
  * predecessor does not end on its candidate), then lz4_decode_blocks checks
  * every block against them.  Streams with truncated matches (whose size
@@ -173,7 +173,7 @@ int lz4r_decompress_device(const void *d_in, size_t in_len, const void *d_block_
  * stream has more blocks than out_cap can hold) when out_cap is too small.
  * One host read-back per pass when out_cap / 300 + 1 <= (in_len - 1) / 8 + 1
  * (the output bounds the block count); a larger out_cap reads the block
- * count back first.  Device scratch: ~20 B per 4 KiB of stream + 8 B per
+ * count back first.  Device scratch: ~20 B per 8 KiB of stream + 8 B per
  * block out_cap can hold (stream-ordered allocation from a per-device pool
  * the library keeps: returned to the pool on return, not to the device, so
  * the next call does not map it again). */

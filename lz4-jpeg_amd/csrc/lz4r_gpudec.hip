@@ -659,7 +659,7 @@ __global__ __launch_bounds__(kLanes) void lz4_decode_blocks(
 // mode parses every block (decode_block<kFindLen>).  The host tries the
 // fast mode first; the decoder checks every block against its boundaries,
 // so a wrong fast-mode boundary is an error, never wrong bytes.
-constexpr int kChunkB = 4096;                        // stream bytes per chunk
+constexpr int kChunkB = 8192;                        // stream bytes per chunk
 constexpr int kWin = 2 * kInMax + 32;                // candidate window (LDS)
 constexpr uint64_t kNone = ~0ull;                    // no candidate in the chunk
 constexpr uint64_t kBad = ~0ull - 1;                 // the walk met an impossible block
